@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""bench.py — fused product+sum-out throughput (factor-entries/s) on MI355X.
+
+Workload (BASELINE config 5 restated): one VE bucket of a
+4-state Potts model,  msg(S_1..S_w, y) = sum_x m(x, S_1..S_w) * f(x, y),  all
+cards k = 4, w = 14, fp32  =>  4^16 = 4.29e9 factor-entries per step, inputs
+resident in HBM.  With --gpus N each rank evaluates its own block of a global
+bucket whose output is split on a leading variable (weak scaling: fixed work
+per GPU, no data-path collective; one barrier + max-reduce of the timer).
+
+A "step" = one fused bucket (one kernel launch) through the C ABI
+(bnpp_bucket_eliminate) on torch's current stream.  Roofline: algorithmic bytes
+= 4 B x (|m| + |f| + |out|) per launch over the kernel's average duration (HIP
+events, same stream) against 8.0 TB/s.  CPU baseline: the reference's own
+Factor::product + Factor::sum_out (oracle/_ref/ref_harness micro, compiled from
+the reference sources), or the oracle restatement if that binary is absent,
+single core, on a bounded sample of the same bucket shape.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "bn-pp_amd", "python"))
+
+METRIC = "factor-entries/sec on fused product+sum-out; MAR wall-clock on 32x32 grid UAI"
+HBM_PEAK = 8.0e12          # B/s, MI355X_MICROARCH.md chip table (spec)
+
+
+def cpu_baseline(k: int, w_cpu: int, reps: int):
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    sample = "m(x,S_1..S_%d)*f(x,y)->sum_x, k=%d, fp64, %d rep(s): %d factor-entries" % (
+        w_cpu, k, reps, k ** (w_cpu + 2) * reps)
+    if os.path.exists(harness):
+        out = subprocess.run(["taskset", "-c", "0", harness, "micro", str(k), str(w_cpu), str(reps)],
+                             capture_output=True, text=True, check=True, timeout=600).stdout
+        kv = dict(line.split() for line in out.splitlines() if len(line.split()) == 2)
+        return {"value": float(kv["entries_per_s"]), "unit": "factor-entries/s", "cores": 1, "kind": "reference",
+                "sample": sample + " (reference Factor::product + sum_out, compiled from /root/reference/code)",
+                "seconds": float(kv["seconds"])}
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import refcpu
+    eps, sec = refcpu.micro_bucket(k, w_cpu, reps)
+    return {"value": eps, "unit": "factor-entries/s", "cores": 1, "kind": "port",
+            "sample": sample + " (oracle restatement)", "seconds": sec}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--w", type=int, default=14)
+    ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--cpu-w", type=int, default=10, help="bucket width of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import bnpp
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    ctx = bnpp.Context(local)
+    dt = bnpp.F32 if args.dtype == "f32" else bnpp.F64
+    tdt = torch.float32 if dt == bnpp.F32 else torch.float64
+    eb = 4 if dt == bnpp.F32 else 8
+    k, w = args.k, args.w
+    S = k ** w
+    # global bucket: variable 0 = L (card world, the leading split variable),
+    # 1 = x, 2..w+1 = S_1..S_w, w+2 = y.  Rank r holds its L = r slice of m and
+    # of the output: views with L conditioned, i.e. a local bucket over (x, S, y).
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    m_t = torch.rand(k * S, generator=g, device=dev, dtype=tdt) * 1.5 + 0.5
+    f_t = torch.rand(k * k, generator=g, device=dev, dtype=tdt) * 1.5 + 0.5
+    out = torch.empty(S * k, device=dev, dtype=tdt)
+    cards = [k] * (w + 2)
+    scope_m, scope_f = list(range(w + 1)), [0, w + 1]
+    out_vars = list(range(1, w + 2))
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        bnpp.bucket_eliminate(ctx, dt, cards, [m_t.data_ptr(), f_t.data_ptr()], [scope_m, scope_f], 0,
+                              out.data_ptr(), out_vars, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    entries = float(k ** (w + 2))                  # prod(card) over (x, S, y), per rank per step
+    value = world * entries * args.steps / elapsed
+    alg_bytes = eb * (k * S + k * k + S * k)       # |m| + |f| + |out|
+    achieved = alg_bytes / (kern_ms * 1e-3)
+
+    # sanity: checksum of checksums (sum_out = sum_x rowsum(m)_x * rowsum(f)_x)
+    M = m_t.double().reshape(k, S)
+    F = f_t.double().reshape(k, k)
+    want = (M.sum(1) * F.sum(1)).sum().item()
+    got = out.double().sum().item()
+    ok = abs(got - want) <= (1e-4 if dt == bnpp.F32 else 1e-9) * want
+
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "traffic_r01.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if tj.get("k") == k and tj.get("w") == w and tj.get("dtype") == args.dtype:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(k, args.cpu_w, args.cpu_reps)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "factor-entries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (U(0.5,2) potentials, seeded)",
+            "config": {"workload": "potts-k%d bucket m(x,S_1..S_%d)*f(x,y)->sum_x (BASELINE config 5 restated, "
+                                   "SURVEY.md 8(d)); output split on a leading variable across ranks" % (k, w),
+                       "k": k, "w": w, "entries_per_gpu_step": entries, "parallelism": "bucket-sharded x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK, "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                         "kernel_ms": kern_ms},
+            "cpu_baseline": cpu,
+            "checksum_ok": ok,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

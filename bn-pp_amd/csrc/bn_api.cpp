@@ -1,0 +1,498 @@
+// C++ mirror of bn-pp's class API (include/bnpp/bn.hpp), layered on the C ABI.
+#include "../../include/bnpp/bn.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <iomanip>
+#include <iostream>
+#include <mutex>
+#include <stdexcept>
+
+#include "../../include/bnpp.h"
+#include "model_io.hpp"
+
+namespace bn {
+namespace {
+
+std::mutex g_mu;
+bnpp_ctx *g_ctx = nullptr;
+int g_device = -1;
+
+bnpp_ctx *ctx() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx) {
+        int dev = g_device;
+        if (dev < 0) {
+            const char *e = std::getenv("BNPP_DEVICE");
+            dev = e ? std::atoi(e) : 0;
+        }
+        if (bnpp_ctx_create(dev, &g_ctx) != BNPP_OK)
+            throw std::runtime_error(std::string("bnpp: cannot create a GPU context: ") + bnpp_last_error());
+    }
+    return g_ctx;
+}
+
+void check(int rc, const char *what) {
+    if (rc != BNPP_OK) throw std::runtime_error(std::string("bnpp: ") + what + ": " + bnpp_last_error());
+}
+
+// RAII device buffer
+struct DevBuf {
+    void *p = nullptr;
+    explicit DevBuf(size_t bytes) { check(bnpp_malloc(ctx(), bytes, &p), "malloc"); }
+    ~DevBuf() { if (p) bnpp_free(ctx(), p); }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+};
+
+std::vector<int> ids(const Domain &d) {
+    std::vector<int> v;
+    for (const Variable *x : d.scope()) v.push_back((int)x->id());
+    return v;
+}
+
+// cardinalities indexed by variable id, covering every listed domain
+std::vector<int> cards_of(std::initializer_list<const Domain *> ds) {
+    std::vector<int> c;
+    for (const Domain *d : ds)
+        for (const Variable *x : d->scope()) {
+            if (c.size() <= x->id()) c.resize(x->id() + 1, 1);
+            c[x->id()] = (int)x->size();
+        }
+    if (c.empty()) c.push_back(1);
+    return c;
+}
+
+double seq_sum(const std::vector<double> &v) {
+    double p = 0;
+    for (double x : v) p += x;
+    return p;
+}
+
+std::vector<double> download(const DevBuf &b, uint64_t n) {
+    std::vector<double> v(n);
+    check(bnpp_synchronize(ctx(), nullptr), "synchronize");
+    check(bnpp_memcpy_d2h(ctx(), v.data(), b.p, n * sizeof(double)), "memcpy d2h");
+    return v;
+}
+
+std::unique_ptr<DevBuf> upload(const std::vector<double> &v) {
+    std::unique_ptr<DevBuf> b(new DevBuf(std::max<size_t>(v.size(), 1) * sizeof(double)));
+    check(bnpp_memcpy_h2d(ctx(), b->p, v.data(), v.size() * sizeof(double)), "memcpy h2d");
+    return b;
+}
+
+int heuristic_of(std::unordered_map<std::string, bool> &o) {      // model.cpp:360, graph.cpp:62-68
+    if (o["min-degree"]) return BNPP_MIN_DEGREE;
+    if (o["weighted-min-fill"]) return BNPP_WEIGHTED_MIN_FILL;
+    if (o["min-fill"]) return BNPP_MIN_FILL;
+    return BNPP_ORDER_GIVEN;
+}
+
+}  // namespace
+
+void set_device(int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_device = device;
+}
+
+std::ostream &operator<<(std::ostream &o, const Variable &v) {
+    return o << "Variable(id:" << v.id() << ", size:" << v.size() << ")";
+}
+
+// ----------------------------------------------------------------- Domain
+Domain::Domain() { init(); }
+Domain::Domain(std::vector<const Variable *> scope) : _scope(std::move(scope)) { init(); }
+Domain::Domain(const Domain &d) : _scope(d._scope) { init(); }
+Domain::Domain(const Domain &d1, const Domain &d2) : _scope(d1._scope) {
+    for (const Variable *v : d2._scope)
+        if (!d1.in_scope(v)) _scope.push_back(v);
+    init();
+}
+Domain::Domain(const Domain &d, const Variable *v) {
+    for (const Variable *x : d._scope)
+        if (x != v) _scope.push_back(x);
+    init();
+}
+Domain::Domain(const Domain &d, const std::unordered_map<unsigned, unsigned> &evidence) {
+    for (const Variable *x : d._scope)
+        if (!evidence.count(x->id())) _scope.push_back(x);
+    init();
+}
+void Domain::init() {
+    _offset.assign(_scope.size(), 1);
+    _size = 1;
+    for (int i = (int)_scope.size() - 1; i >= 0; --i) {
+        _offset[i] = _size;
+        _size *= _scope[i]->size();
+    }
+}
+const Variable *Domain::operator[](unsigned i) const {
+    if (i < _scope.size()) return _scope[i];
+    throw "Domain::operator[unsigned i]: Index out of range!";
+}
+bool Domain::in_scope(const Variable *v) const { return in_scope(v->id()); }
+bool Domain::in_scope(unsigned id) const {
+    for (const Variable *x : _scope)
+        if (x->id() == id) return true;
+    return false;
+}
+void Domain::next_valuation(std::vector<unsigned> &val) const {
+    int j;
+    for (j = (int)val.size() - 1; j >= 0 && val[j] == _scope[j]->size() - 1; --j) val[j] = 0;
+    if (j >= 0) val[j]++;
+}
+uint64_t Domain::position_valuation(const std::vector<unsigned> &val) const {
+    uint64_t pos = 0;
+    for (size_t i = 0; i < _scope.size(); ++i) pos += val[i] * _offset[i];
+    return pos;
+}
+uint64_t Domain::position_consistent_valuation(const std::vector<unsigned> &val, const Domain &domain) const {
+    uint64_t pos = 0;
+    for (size_t i = 0; i < _scope.size(); ++i)
+        for (size_t j = 0; j < domain._scope.size(); ++j)
+            if (domain._scope[j]->id() == _scope[i]->id()) pos += _offset[i] * val[j];
+    return pos;
+}
+std::ostream &operator<<(std::ostream &o, const Domain &d) {
+    o << "Domain{";
+    for (unsigned i = 0; i < d.width(); ++i) o << (i ? ", " : "") << d._scope[i]->id();
+    return o << "}";
+}
+
+// ----------------------------------------------------------------- Factor
+Factor::Factor(const Domain *domain, std::vector<double> values, double partition)
+    : _domain(domain), _values(std::move(values)), _partition(partition) {}
+Factor::Factor(const Domain *domain, double value)
+    : _domain(domain), _values(domain->size(), value), _partition(domain->size() * value) {}
+Factor::Factor(double value) : _domain(new Domain()), _values(1, value), _partition(value) {}
+Factor::Factor(const Factor &f) : _domain(new Domain(*f._domain)), _values(f._values), _partition(f._partition) {}
+Factor::Factor(Factor &&f) noexcept : _domain(f._domain), _values(std::move(f._values)), _partition(f._partition) {
+    f._domain = nullptr;
+    f._partition = 0.0;
+}
+Factor::~Factor() { delete _domain; }
+Factor &Factor::operator=(Factor &&f) noexcept {
+    if (this != &f) {
+        delete _domain;
+        _domain = f._domain;
+        _values = std::move(f._values);
+        _partition = f._partition;
+        f._domain = nullptr;
+        f._partition = 0.0;
+    }
+    return *this;
+}
+Factor &Factor::operator=(const Factor &f) {
+    if (this != &f) {
+        Factor c(f);
+        *this = std::move(c);
+    }
+    return *this;
+}
+Factor Factor::operator*(const Factor &f) { return product(f); }
+void Factor::operator*=(const Factor &f) { *this = product(f); }
+const double &Factor::operator[](uint64_t i) const {
+    if (i < size()) return _values.at(i);
+    throw "Factor::operator[]: Index out of range.";
+}
+double &Factor::operator[](uint64_t i) {
+    if (i < size()) return _values[i];
+    throw "Factor::operator[]: Index out of range.";
+}
+double Factor::max() const {
+    double m = 0.0;
+    for (double p : _values) m = p > m ? p : m;
+    return m;
+}
+double Factor::min() const {
+    double m = _partition;
+    for (double p : _values) m = p < m ? p : m;
+    return m;
+}
+
+Factor Factor::product(const Factor &f) const {
+    Domain *nd = new Domain(*_domain, *f._domain);
+    std::vector<int> cards = cards_of({_domain, f._domain});
+    auto a = upload(_values), b = upload(f._values);
+    DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
+    std::vector<int> av = ids(*_domain), bv = ids(*f._domain), ov = ids(*nd);
+    check(bnpp_product(ctx(), nullptr, BNPP_F64, cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
+                       bv.data(), out.p, (int)ov.size(), ov.data()),
+          "product");
+    std::vector<double> vals = download(out, nd->size());
+    double p = seq_sum(vals);
+    return Factor(nd, std::move(vals), p);
+}
+
+Factor Factor::sum_out(const Variable *variable) const {
+    if (!_domain->in_scope(variable)) return Factor(*this);       // factor.cpp:185-188
+    Domain *nd = new Domain(*_domain, variable);
+    std::vector<int> cards = cards_of({_domain});
+    auto a = upload(_values);
+    DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
+    std::vector<int> av = ids(*_domain), ov = ids(*nd);
+    check(bnpp_sum_out(ctx(), nullptr, BNPP_F64, cards.data(), a->p, (int)av.size(), av.data(), (int)variable->id(),
+                       out.p, (int)ov.size(), ov.data()),
+          "sum_out");
+    std::vector<double> vals = download(out, nd->size());
+    double p = seq_sum(vals);
+    return Factor(nd, std::move(vals), p);
+}
+
+Factor Factor::conditioning(const std::unordered_map<unsigned, unsigned> &evidence) const {
+    Domain *nd = new Domain(*_domain, evidence);
+    std::vector<int> cards = cards_of({_domain});
+    std::vector<int> ev_vars, ev_vals;
+    for (auto &kv : evidence) {
+        ev_vars.push_back((int)kv.first);
+        ev_vals.push_back((int)kv.second);
+    }
+    auto a = upload(_values);
+    DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
+    std::vector<int> av = ids(*_domain);
+    check(bnpp_condition(ctx(), nullptr, BNPP_F64, cards.data(), a->p, (int)av.size(), av.data(), (int)ev_vars.size(),
+                         ev_vars.data(), ev_vals.data(), out.p),
+          "conditioning");
+    std::vector<double> vals = download(out, nd->size());
+    double p = seq_sum(vals);
+    return Factor(nd, std::move(vals), p);
+}
+
+Factor Factor::normalize() const {
+    Factor f(*this);
+    for (double &v : f._values) v = v / f._partition;
+    f._partition = 1.0;
+    return f;
+}
+
+std::ostream &operator<<(std::ostream &os, const Factor &f) {      // factor.cpp:291-321
+    const Domain &d = *f._domain;
+    os << "Factor(width:" << f.width() << ", size:" << f.size() << ", partition:" << f._partition << ")" << std::endl;
+    for (unsigned i = 0; i < d.width(); ++i) os << d[i]->id() << " ";
+    os << std::endl;
+    std::vector<unsigned> val(d.width(), 0);
+    for (uint64_t i = 0; i < f.size(); ++i) {
+        for (unsigned j = 0; j < d.width(); ++j) os << val[j] << " ";
+        os << ": " << std::fixed << std::setprecision(7) << f._values[i] << std::endl;
+        d.next_valuation(val);
+    }
+    return os;
+}
+
+// ------------------------------------------------------------------ models
+namespace {
+
+bnpp_model *to_engine(const std::vector<Variable *> &vars, const std::vector<const Factor *> &factors) {
+    std::vector<int> cards, widths, scopes;
+    std::vector<double> values;
+    for (const Variable *v : vars) {
+        if (cards.size() <= v->id()) cards.resize(v->id() + 1, 1);
+        cards[v->id()] = (int)v->size();
+    }
+    for (const Factor *f : factors) {
+        widths.push_back((int)f->width());
+        for (const Variable *x : f->domain().scope()) scopes.push_back((int)x->id());
+        values.insert(values.end(), f->values().begin(), f->values().end());
+    }
+    bnpp_model *m = nullptr;
+    check(bnpp_model_from_arrays(0, (int)cards.size(), cards.data(), (int)factors.size(), widths.data(), scopes.data(),
+                                 values.data(), &m),
+          "model");
+    return m;
+}
+
+struct ModelGuard {
+    bnpp_model *m;
+    ~ModelGuard() { bnpp_model_free(m); }
+};
+
+void split_evidence(const std::unordered_map<unsigned, unsigned> &ev, std::vector<int> &vars, std::vector<int> &vals) {
+    for (auto &kv : ev) {
+        vars.push_back((int)kv.first);
+        vals.push_back((int)kv.second);
+    }
+}
+
+}  // namespace
+
+Model::Model(std::string name, std::vector<Variable *> &variables, std::vector<Factor *> &factors)
+    : _name(std::move(name)), _variables(variables), _factors(factors) {}
+
+Model::~Model() {
+    for (auto pv : _variables) delete pv;
+    for (auto pf : _factors) delete pf;
+}
+
+double Model::log10_partition(const std::unordered_map<unsigned, unsigned> &evidence,
+                              std::unordered_map<std::string, bool> &options, double &uptime) const {
+    auto t0 = std::chrono::steady_clock::now();
+    ModelGuard g{to_engine(_variables, std::vector<const Factor *>(_factors.begin(), _factors.end()))};
+    std::vector<int> ev_vars, ev_vals;
+    split_evidence(evidence, ev_vars, ev_vals);
+    double lz = 0, z = 0, up = 0;
+    int dt = options["fp32"] ? BNPP_F32 : BNPP_F64;
+    check(bnpp_partition(ctx(), g.m, (int)ev_vars.size(), ev_vars.data(), ev_vals.data(), heuristic_of(options),
+                         nullptr, 0, dt, &lz, &z, &up),
+          "partition");
+    uptime = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return lz;
+}
+
+double Model::partition(const std::unordered_map<unsigned, unsigned> &evidence,
+                        std::unordered_map<std::string, bool> &options, double &uptime) const {
+    auto t0 = std::chrono::steady_clock::now();
+    ModelGuard g{to_engine(_variables, std::vector<const Factor *>(_factors.begin(), _factors.end()))};
+    std::vector<int> ev_vars, ev_vals;
+    split_evidence(evidence, ev_vars, ev_vals);
+    double lz = 0, z = 0, up = 0;
+    int dt = options["fp32"] ? BNPP_F32 : BNPP_F64;
+    check(bnpp_partition(ctx(), g.m, (int)ev_vars.size(), ev_vars.data(), ev_vals.data(), heuristic_of(options),
+                         nullptr, 0, dt, &lz, &z, &up),
+          "partition");
+    uptime = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return z;                                        // part.partition() (model.cpp:289)
+}
+
+std::vector<const Factor *> Model::marginals(const std::unordered_map<unsigned, unsigned> &evidence,
+                                             std::unordered_map<std::string, bool> &options, double &uptime) const {
+    auto t0 = std::chrono::steady_clock::now();
+    ModelGuard g{to_engine(_variables, std::vector<const Factor *>(_factors.begin(), _factors.end()))};
+    std::vector<int> ev_vars, ev_vals;
+    split_evidence(evidence, ev_vars, ev_vals);
+    size_t total = 0;
+    for (auto pv : _variables) total += pv->size();
+    std::vector<double> out(total);
+    std::vector<int> targets;
+    for (auto pv : _variables) targets.push_back((int)pv->id());
+    double up = 0;
+    int dt = options["fp32"] ? BNPP_F32 : BNPP_F64;
+    check(bnpp_marginals(ctx(), g.m, (int)ev_vars.size(), ev_vars.data(), ev_vals.data(), heuristic_of(options),
+                         (int)targets.size(), targets.data(), dt, out.data(), &up),
+          "marginals");
+    std::vector<const Factor *> marg;
+    size_t o = 0;
+    for (auto pv : _variables) {
+        if (evidence.count(pv->id())) {               // width-0 factor with value 1 (model.cpp:333)
+            marg.push_back(new Factor(new Domain(), std::vector<double>{1.0}, 1.0));
+        } else {
+            std::vector<double> v(out.begin() + o, out.begin() + o + pv->size());
+            marg.push_back(new Factor(new Domain(std::vector<const Variable *>{pv}), v, 1.0));
+        }
+        o += pv->size();
+    }
+    uptime = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return marg;
+}
+
+BN::BN(std::string name, std::vector<Variable *> &variables, std::vector<Factor *> &factors)
+    : Model(std::move(name), variables, factors) {
+    for (auto pv : _variables) _children[pv] = {};
+    for (size_t i = 0; i < _variables.size() && i < _factors.size(); ++i) {   // model.cpp:111-119
+        const Variable *v = _variables[i];
+        std::vector<const Variable *> scope = _factors[i]->domain().scope();
+        std::unordered_set<const Variable *> parents;
+        if (!scope.empty()) parents.insert(scope.begin() + 1, scope.end());
+        _parents[v] = parents;
+        for (auto p : parents) _children[p].insert(v);
+    }
+}
+
+Factor BN::variable_elimination(std::vector<const Variable *> &variables, std::vector<const Factor *> &factors,
+                                std::unordered_map<std::string, bool> &options) const {
+    ModelGuard g{to_engine(_variables, factors)};
+    std::vector<int> vars;
+    for (auto pv : variables) vars.push_back((int)pv->id());
+    int cap_vars = (int)_variables.size() + 1;
+    std::vector<int> out_vars(cap_vars);
+    int ndims = 0;
+    int64_t size = 0, exp2 = 0;
+    // the result scope is what no bucket eliminated: at most every variable
+    uint64_t cap = 1;
+    for (auto f : factors) cap = std::max<uint64_t>(cap, f->size());
+    std::vector<double> vals;
+    int dt = options["fp32"] ? BNPP_F32 : BNPP_F64;
+    int h = heuristic_of(options);
+    for (;;) {
+        vals.assign(cap, 0.0);
+        int rc = bnpp_variable_elimination(ctx(), g.m, (int)vars.size(), vars.data(), h, dt, cap_vars, &ndims,
+                                           out_vars.data(), (int64_t)cap, &size, vals.data(), &exp2);
+        if (rc == BNPP_OK) break;
+        if ((uint64_t)size > cap) { cap = (uint64_t)size; continue; }
+        check(rc, "variable_elimination");
+    }
+    vals.resize((size_t)size);
+    for (double &v : vals) v = std::ldexp(v, (int)exp2);
+    std::vector<const Variable *> scope;
+    for (int i = 0; i < ndims; ++i)
+        for (auto pv : _variables)
+            if ((int)pv->id() == out_vars[i]) scope.push_back(pv);
+    double p = seq_sum(vals);
+    return Factor(new Domain(scope), std::move(vals), p);
+}
+
+MN::MN(std::string name, std::vector<Variable *> &variables, std::vector<Factor *> &factors)
+    : Model(std::move(name), variables, factors) {}
+
+// -------------------------------------------------------------------- I/O
+namespace {
+int read_any(std::string &filename, bnpp::ModelData &d) {
+    std::string err;
+    int rc = bnpp::load_uai(filename, d, &err);
+    if (rc) std::cerr << "Error: " << err << std::endl;
+    return rc;
+}
+void materialise(const bnpp::ModelData &d, std::vector<Variable *> &vars, std::vector<Factor *> &factors) {
+    for (size_t i = 0; i < d.cards.size(); ++i) vars.push_back(new Variable((unsigned)i, (unsigned)d.cards[i]));
+    for (size_t f = 0; f < d.scopes.size(); ++f) {
+        std::vector<const Variable *> scope;
+        for (int v : d.scopes[f]) scope.push_back(vars[v]);
+        double p = seq_sum(d.values[f]);
+        factors.push_back(new Factor(new Domain(scope), d.values[f], p));
+    }
+}
+}  // namespace
+
+int read_uai_model(std::string &filename, BN **model) {            // io.cpp:102-127
+    bnpp::ModelData d;
+    int rc = read_any(filename, d);
+    if (rc) return rc;
+    if (!d.is_bayes) {
+        std::cerr << "Error: file " << filename << " is not a BAYES net." << std::endl;
+        return -2;
+    }
+    std::vector<Variable *> vars;
+    std::vector<Factor *> factors;
+    materialise(d, vars, factors);
+    *model = new BN(filename, vars, factors);
+    return 0;
+}
+
+int read_uai_model(std::string &filename, MN **model) {            // io.cpp:129-154
+    bnpp::ModelData d;
+    int rc = read_any(filename, d);
+    if (rc) return rc;
+    if (d.is_bayes) {
+        std::cerr << "Error: file " << filename << " is not a MARKOV net." << std::endl;
+        return -2;
+    }
+    std::vector<Variable *> vars;
+    std::vector<Factor *> factors;
+    materialise(d, vars, factors);
+    *model = new MN(filename, vars, factors);
+    return 0;
+}
+
+int read_uai_evidence(std::string &filename, std::unordered_map<unsigned, unsigned> &evidence) {   // io.cpp:157-180
+    std::vector<std::pair<int, int>> ev;
+    if (bnpp::load_evidence(filename, ev)) {
+        std::cerr << "Error: couldn't read file " << filename << std::endl;
+        return -1;
+    }
+    for (auto &p : ev) evidence[(unsigned)p.first] = (unsigned)p.second;
+    return 0;
+}
+
+}  // namespace bn

@@ -1,0 +1,83 @@
+// bnpp — command-line front end with the reference's task flags (bn.cpp:136-258,
+// mn.cpp:135-155): -pr / -mar, -mf / -wmf / -md, -v, plus -f32.  BAYES files
+// print like `bn` (raw Z), MARKOV files like `mn` (log10 Z).
+#include <cmath>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/bnpp/bn.hpp"
+#include "../../include/bnpp.h"
+
+int main(int argc, char **argv) {
+    std::unordered_map<std::string, bool> options;
+    std::vector<std::string> positional;
+    for (int i = 1; i < argc; ++i) {
+        std::string p(argv[i]);
+        if (p == "-pr") options["partition"] = true;
+        else if (p == "-mar") options["marginals"] = true;
+        else if (p == "-ve") options["variable-elimination"] = true;
+        else if (p == "-mf") options["min-fill"] = true;
+        else if (p == "-wmf") options["weighted-min-fill"] = true;
+        else if (p == "-md") options["min-degree"] = true;
+        else if (p == "-f32") options["fp32"] = true;
+        else if (p == "-v") options["verbose"] = true;
+        else if (p == "-h") options["help"] = true;
+        else if (p[0] == '-') { std::cerr << "Error: invalid option `" << p << "'." << std::endl; return -1; }
+        else positional.push_back(p);
+    }
+    if (positional.empty() || options["help"]) {
+        std::cout << "usage: " << argv[0] << " /path/to/model.uai [/path/to/evidence.uai.evid] -pr|-mar [-mf|-wmf|-md] [-f32]" << std::endl;
+        return positional.empty() ? 1 : 0;
+    }
+    bnpp_model *probe = nullptr;
+    if (bnpp_model_load_uai(positional[0].c_str(), &probe) != BNPP_OK) {
+        std::cerr << "Error: " << bnpp_last_error() << std::endl;
+        return -1;
+    }
+    int is_bayes = 0;
+    bnpp_model_info(probe, &is_bayes, nullptr, nullptr);
+    bnpp_model_free(probe);
+    std::unordered_map<unsigned, unsigned> evidence;
+    if (positional.size() > 1 && bn::read_uai_evidence(positional[1], evidence)) return -2;
+    bn::Model *model = nullptr;
+    if (is_bayes) {
+        bn::BN *m = nullptr;
+        if (bn::read_uai_model(positional[0], &m)) return -1;
+        model = m;
+    } else {
+        bn::MN *m = nullptr;
+        if (bn::read_uai_model(positional[0], &m)) return -1;
+        model = m;
+    }
+    try {
+        double uptime = 0;
+        if (options["partition"]) {
+            if (is_bayes) {
+                double p = model->partition(evidence, options, uptime);
+                std::cout << ">> Partition = " << p << std::endl;
+            } else {
+                double p = model->log10_partition(evidence, options, uptime);
+                std::cout << "Partition = " << p << std::endl << std::endl;
+            }
+            std::cout << ">> Executed in " << uptime << "ms." << std::endl << std::endl;
+        }
+        if (options["marginals"]) {
+            std::vector<const bn::Factor *> marg = model->marginals(evidence, options, uptime);
+            std::cout << ">> Marginals:" << std::endl;
+            for (auto pf : marg) {
+                std::cout << *pf << std::endl;
+                delete pf;
+            }
+            std::cout << ">> Executed in " << uptime << "ms." << std::endl << std::endl;
+        }
+    } catch (const std::exception &e) {
+        std::cerr << "Error: " << e.what() << std::endl;
+        delete model;
+        return -3;
+    }
+    delete model;
+    return 0;
+}

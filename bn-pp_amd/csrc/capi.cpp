@@ -1,0 +1,711 @@
+// extern "C" boundary (include/bnpp.h).  No exception crosses it: every entry
+// point catches, records bnpp_last_error() and returns a status code.
+#include "../../include/bnpp.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "model_io.hpp"
+#include "order.hpp"
+#include "plan.hpp"
+#include "runtime.hpp"
+
+using namespace bnpp;
+
+struct bnpp_ctx {
+    Context c;
+};
+struct bnpp_model {
+    ModelData d;
+};
+struct bnpp_job {
+    bnpp_ctx *ctx = nullptr;
+    int kind = 0;
+    DeviceSources src;
+    Executable ex;
+    std::vector<int> targets;
+    std::vector<int> ev_val;          // per variable, -1 = no evidence
+    std::vector<int> cards;
+    double stats[8] = {0};
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int status, const std::string &msg) {
+    g_err = msg;
+    return status;
+}
+int from_ctx(bnpp_ctx *ctx, int rc) {
+    if (rc == 0) return BNPP_OK;
+    g_err = ctx->c.last_error;
+    return rc == -3 ? BNPP_ERR_OOM : rc == -1 ? BNPP_ERR_INVALID : BNPP_ERR_HIP;
+}
+hipStream_t pick_stream(bnpp_ctx *ctx, void *stream) {
+    return stream ? static_cast<hipStream_t>(stream) : ctx->c.stream;
+}
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+#define BNPP_GUARD_BEGIN try {
+#define BNPP_GUARD_END                                                       \
+    }                                                                        \
+    catch (const std::bad_alloc &) {                                         \
+        return set_err(BNPP_ERR_OOM, "host out of memory");                  \
+    }                                                                        \
+    catch (const std::exception &e) {                                        \
+        return set_err(BNPP_ERR_INVALID, e.what());                          \
+    }                                                                        \
+    catch (...) {                                                            \
+        return set_err(BNPP_ERR_INVALID, "unknown error");                   \
+    }
+
+bool valid_scope(int ndims, const int *vars, const int *cards, int ncards_hint) {
+    (void)ncards_hint;
+    if (ndims < 0 || (ndims > 0 && !vars)) return false;
+    for (int i = 0; i < ndims; ++i) {
+        if (vars[i] < 0 || cards[vars[i]] < 1) return false;
+        for (int j = 0; j < i; ++j)
+            if (vars[j] == vars[i]) return false;
+    }
+    return true;
+}
+
+int max_vec_for(int dtype) { return dtype == BNPP_F32 ? 4 : 2; }
+
+// Launch one bucket with the descriptor in the kernel-argument segment.
+int run_single(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &cards, const BucketSpec &b,
+               const std::vector<const void *> &in_ptrs, void *out) {
+    if (dtype != BNPP_F32 && dtype != BNPP_F64) return set_err(BNPP_ERR_INVALID, "dtype must be BNPP_F64 or BNPP_F32");
+    SingleArgs a;
+    std::memset(&a, 0, sizeof a);
+    std::vector<int64_t> pool;
+    std::string msg;
+    if (!build_desc(b, cards, max_vec_for(dtype), a.d, pool, &msg)) return set_err(BNPP_ERR_INVALID, msg);
+    if (pool.size() > (size_t)kMaxPool)
+        return set_err(BNPP_ERR_UNSUPPORTED, "too many non-mergeable output dims for a single-op call");
+    std::copy(pool.begin(), pool.end(), a.pool);
+    a.d.dim_off = 0;
+    for (size_t i = 0; i < in_ptrs.size(); ++i) a.meta[i].ptr = const_cast<void *>(in_ptrs[i]);
+    a.meta[in_ptrs.size()].ptr = out;
+    hipError_t e = hipSetDevice(ctx->c.device);
+    if (e == hipSuccess) e = launch_single(dtype == BNPP_F32, a, ctx->c.max_grid, pick_stream(ctx, stream));
+    if (e != hipSuccess) return set_err(BNPP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    return BNPP_OK;
+}
+
+// evidence as a per-variable array (-1: none); validates ids and values
+bool evidence_array(const ModelData &d, int n_ev, const int *ev_vars, const int *ev_vals, std::vector<int> &ev,
+                    std::string &msg) {
+    ev.assign(d.cards.size(), -1);
+    if (n_ev < 0 || (n_ev > 0 && (!ev_vars || !ev_vals))) {
+        msg = "bad evidence arrays";
+        return false;
+    }
+    for (int i = 0; i < n_ev; ++i) {
+        int v = ev_vars[i], x = ev_vals[i];
+        if (v < 0 || v >= (int)d.cards.size() || x < 0 || x >= d.cards[v]) {
+            msg = "evidence out of range";
+            return false;
+        }
+        ev[v] = x;                          // evidence[id] = val (io.cpp:171)
+    }
+    return true;
+}
+
+std::vector<std::vector<int>> conditioned_scopes(const ModelData &d, const std::vector<int> &ev) {
+    std::vector<std::vector<int>> sc(d.scopes.size());
+    for (size_t f = 0; f < d.scopes.size(); ++f)
+        for (int v : d.scopes[f])
+            if (ev[v] < 0) sc[f].push_back(v);
+    return sc;
+}
+
+std::vector<View> source_views(const ModelData &d, const std::vector<int> &ev) {
+    std::vector<View> views;
+    for (size_t f = 0; f < d.scopes.size(); ++f) views.push_back(conditioned_view((int)f, d.scopes[f], d.cards, ev));
+    return views;
+}
+
+// Build the VE plans for a job: kind 0 = partition, kind 1 = marginals of targets.
+int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
+                int n_order, const std::vector<int> &targets, std::vector<VEPlan> &plans, int &max_width) {
+    const int nv = (int)d.cards.size();
+    auto scopes = conditioned_scopes(d, ev);
+    auto views = source_views(d, ev);
+    max_width = 0;
+    if (heuristic < BNPP_ORDER_GIVEN || heuristic > BNPP_MIN_DEGREE)
+        return set_err(BNPP_ERR_INVALID, "unknown heuristic");
+    if (kind == 2) {                                     // caller-chosen variables
+        std::vector<int> vars(order, order + n_order), ord;
+        for (int v : vars)
+            if (v < 0 || v >= nv) return set_err(BNPP_ERR_INVALID, "bad variable");
+        max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
+        plans.push_back(plan_ve(d.cards, views, ord, true));
+    } else if (kind == 0) {
+        std::vector<int> vars, ord;
+        if (order) {
+            std::vector<char> seen(nv, 0);
+            for (int i = 0; i < n_order; ++i) {
+                int v = order[i];
+                if (v < 0 || v >= nv || seen[v]) return set_err(BNPP_ERR_INVALID, "bad explicit order");
+                seen[v] = 1;
+                if (ev[v] < 0) vars.push_back(v);
+            }
+            ord = vars;
+            max_width = order_width(nv, scopes, ord);
+        } else {
+            for (int v = 0; v < nv; ++v)
+                if (ev[v] < 0) vars.push_back(v);        // model.cpp:277-282
+            max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
+        }
+        plans.push_back(plan_ve(d.cards, views, ord, true));
+    } else {
+        for (int t : targets) {
+            std::vector<int> vars, ord;
+            for (int v = 0; v < nv; ++v)                 // model.cpp:327-332 (evidence vars are no-ops)
+                if (v != t && ev[v] < 0) vars.push_back(v);
+            int w = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
+            max_width = std::max(max_width, w);
+            plans.push_back(plan_ve(d.cards, views, ord, true));
+        }
+    }
+    return BNPP_OK;
+}
+
+int plan_schedule(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
+                  int n_order, const std::vector<int> &targets, int dtype, Schedule &s, double *stats) {
+    std::vector<VEPlan> plans;
+    int width = 0;
+    int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width);
+    if (rc) return rc;
+    std::vector<const VEPlan *> pp;
+    for (auto &p : plans) pp.push_back(&p);
+    std::vector<int64_t> src_sizes;
+    for (auto &v : d.values) src_sizes.push_back((int64_t)v.size());
+    const int eb = dtype == BNPP_F32 ? 4 : 8;
+    std::string msg;
+    if (!build_schedule(pp, d.cards, src_sizes, eb, max_vec_for(dtype), s, &msg)) return set_err(BNPP_ERR_INVALID, msg);
+    stats[0] = s.entries;
+    stats[1] = (double)s.arena_bytes;
+    stats[2] = (double)s.level_vblocks.size();
+    stats[3] = (double)s.descs.size();
+    stats[4] = width;
+    int64_t mx = 0;
+    for (auto &p : plans) mx = std::max(mx, p.max_table);
+    stats[5] = (double)mx;
+    stats[6] = s.elems_moved * eb;
+    return BNPP_OK;
+}
+
+int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals,
+               int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
+               std::unique_ptr<bnpp_job> &job) {
+    if (!ctx || !m) return set_err(BNPP_ERR_INVALID, "null context or model");
+    if (dtype != BNPP_F32 && dtype != BNPP_F64) return set_err(BNPP_ERR_INVALID, "bad dtype");
+    const ModelData &d = m->d;
+    job.reset(new bnpp_job);
+    job->ctx = ctx;
+    job->kind = kind;
+    job->cards = d.cards;
+    std::string msg;
+    if (!evidence_array(d, n_ev, ev_vars, ev_vals, job->ev_val, msg)) return set_err(BNPP_ERR_INVALID, msg);
+    if (kind == 1) {
+        if (targets) {
+            for (int i = 0; i < n_targets; ++i) {
+                if (targets[i] < 0 || targets[i] >= (int)d.cards.size()) return set_err(BNPP_ERR_INVALID, "bad target");
+                job->targets.push_back(targets[i]);
+            }
+        } else {
+            for (int v = 0; v < (int)d.cards.size(); ++v) job->targets.push_back(v);
+        }
+    }
+    Schedule s;
+    int rc = plan_schedule(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, s, job->stats);
+    if (rc) return rc;
+    rc = upload_sources(ctx->c, d.values, dtype == BNPP_F32 ? kF32 : kF64, job->src);
+    if (rc) return from_ctx(ctx, rc);
+    rc = make_executable(ctx->c, job->src, std::move(s), job->ex);
+    if (rc) return from_ctx(ctx, rc);
+    return BNPP_OK;
+}
+
+void destroy_job(bnpp_job *job) {
+    if (!job) return;
+    (void)hipSetDevice(job->ctx->c.device);
+    free_executable(job->ex);
+    free_sources(job->src);
+    delete job;
+}
+
+// results of a launched job: partition -> out[0] = log10 Z (z_out: Z);
+// marginals -> sum(card) normalised values
+int job_results(bnpp_job *job, hipStream_t stream, double *out, double *z_out) {
+    std::vector<std::vector<double>> vals;
+    std::vector<int64_t> exp2;
+    int rc = fetch_results(job->ctx->c, job->ex, stream, vals, exp2);
+    if (rc) return from_ctx(job->ctx, rc);
+    if (job->kind == 0) {
+        double p = 0;                                   // part.partition(): sequential sum
+        for (double v : vals[0]) p += v;
+        out[0] = p > 0 ? std::log10(p) + (double)exp2[0] * std::log10(2.0) : -INFINITY;
+        if (z_out) *z_out = std::ldexp(p, (int)std::max<int64_t>(std::min<int64_t>(exp2[0], 1 << 20), -(1 << 20)));
+        return BNPP_OK;
+    }
+    size_t o = 0;
+    for (size_t i = 0; i < job->targets.size(); ++i) {
+        int t = job->targets[i];
+        int k = job->cards[t];
+        const std::vector<double> &r = vals[i];
+        if (job->ev_val[t] >= 0) {                      // evidence variable: one-hot
+            for (int s = 0; s < k; ++s) out[o + s] = s == job->ev_val[t] ? 1.0 : 0.0;
+        } else if ((int)r.size() == k && k > 0 && job->ex.sched.plan_result_vars[i].size() == 1) {
+            double part = 0;                            // Factor::normalize (factor.cpp:244-255)
+            for (double v : r) part += v;
+            for (int s = 0; s < k; ++s) out[o + s] = r[s] / part;
+        } else {                                        // variable in no factor
+            for (int s = 0; s < k; ++s) out[o + s] = 1.0 / k;
+        }
+        o += (size_t)k;
+    }
+    return BNPP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *bnpp_strerror(int status) {
+    switch (status) {
+        case BNPP_OK: return "ok";
+        case BNPP_ERR_INVALID: return "invalid argument or shape";
+        case BNPP_ERR_NO_DEVICE: return "no usable GPU device";
+        case BNPP_ERR_OOM: return "out of memory";
+        case BNPP_ERR_HIP: return "HIP runtime error";
+        case BNPP_ERR_IO: return "cannot read or parse file";
+        case BNPP_ERR_UNSUPPORTED: return "unsupported shape";
+        default: return "unknown status";
+    }
+}
+
+const char *bnpp_last_error(void) { return g_err.c_str(); }
+int bnpp_version(void) { return BNPP_VERSION; }
+
+int bnpp_device_count(int *n) {
+    if (!n) return set_err(BNPP_ERR_INVALID, "null output");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = e == hipSuccess ? c : 0;
+    return BNPP_OK;
+}
+
+int bnpp_ctx_create(int device, bnpp_ctx **out) {
+    BNPP_GUARD_BEGIN
+    if (!out) return set_err(BNPP_ERR_INVALID, "null output");
+    *out = nullptr;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess || c <= 0) return set_err(BNPP_ERR_NO_DEVICE, "no HIP device visible (the engine has no CPU fallback)");
+    if (device < 0 || device >= c) return set_err(BNPP_ERR_NO_DEVICE, "device index out of range");
+    if ((e = hipSetDevice(device)) != hipSuccess) return set_err(BNPP_ERR_HIP, hipGetErrorString(e));
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return set_err(BNPP_ERR_HIP, hipGetErrorString(e));
+    std::unique_ptr<bnpp_ctx> ctx(new bnpp_ctx);
+    ctx->c.device = device;
+    ctx->c.max_grid = prop.multiProcessorCount * 8;
+    if ((e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(BNPP_ERR_HIP, hipGetErrorString(e));
+    *out = ctx.release();
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_ctx_destroy(bnpp_ctx *ctx) {
+    if (!ctx) return BNPP_OK;
+    (void)hipSetDevice(ctx->c.device);
+    if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
+    delete ctx;
+    return BNPP_OK;
+}
+
+int bnpp_ctx_stream(bnpp_ctx *ctx, void **stream) {
+    if (!ctx || !stream) return set_err(BNPP_ERR_INVALID, "null argument");
+    *stream = ctx->c.stream;
+    return BNPP_OK;
+}
+
+int bnpp_malloc(bnpp_ctx *ctx, size_t bytes, void **dptr) {
+    if (!ctx || !dptr) return set_err(BNPP_ERR_INVALID, "null argument");
+    (void)hipSetDevice(ctx->c.device);
+    hipError_t e = hipMalloc(dptr, bytes ? bytes : 1);
+    if (e != hipSuccess) return set_err(e == hipErrorOutOfMemory ? BNPP_ERR_OOM : BNPP_ERR_HIP, hipGetErrorString(e));
+    return BNPP_OK;
+}
+
+int bnpp_free(bnpp_ctx *ctx, void *dptr) {
+    if (!ctx) return set_err(BNPP_ERR_INVALID, "null context");
+    (void)hipSetDevice(ctx->c.device);
+    hipError_t e = hipFree(dptr);
+    return e == hipSuccess ? BNPP_OK : set_err(BNPP_ERR_HIP, hipGetErrorString(e));
+}
+
+int bnpp_memcpy_h2d(bnpp_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (!ctx) return set_err(BNPP_ERR_INVALID, "null context");
+    (void)hipSetDevice(ctx->c.device);
+    hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    return e == hipSuccess ? BNPP_OK : set_err(BNPP_ERR_HIP, hipGetErrorString(e));
+}
+
+int bnpp_memcpy_d2h(bnpp_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (!ctx) return set_err(BNPP_ERR_INVALID, "null context");
+    (void)hipSetDevice(ctx->c.device);
+    hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? BNPP_OK : set_err(BNPP_ERR_HIP, hipGetErrorString(e));
+}
+
+int bnpp_synchronize(bnpp_ctx *ctx, void *stream) {
+    if (!ctx) return set_err(BNPP_ERR_INVALID, "null context");
+    (void)hipSetDevice(ctx->c.device);
+    hipError_t e = hipStreamSynchronize(pick_stream(ctx, stream));
+    return e == hipSuccess ? BNPP_OK : set_err(BNPP_ERR_HIP, hipGetErrorString(e));
+}
+
+int bnpp_out_scope(int n_in, const int *in_ndims, const int *const *in_vars, int elim_var, int cap,
+                   int *out_ndims, int *out_vars) {
+    BNPP_GUARD_BEGIN
+    if (n_in < 0 || (n_in > 0 && (!in_ndims || !in_vars)) || !out_ndims) return set_err(BNPP_ERR_INVALID, "bad arguments");
+    std::vector<int> u;
+    for (int i = 0; i < n_in; ++i) {
+        std::vector<int> s(in_vars[i], in_vars[i] + in_ndims[i]);
+        u = union_scope(u, s);
+    }
+    if (elim_var >= 0) u = remove_var(u, elim_var);
+    *out_ndims = (int)u.size();
+    if ((int)u.size() > cap) return set_err(BNPP_ERR_INVALID, "output scope larger than cap");
+    std::copy(u.begin(), u.end(), out_vars);
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, int n_in,
+                          const void *const *in_tables, const int *in_ndims, const int *const *in_vars, int elim_var,
+                          void *out_table, int out_ndims, const int *out_vars) {
+    BNPP_GUARD_BEGIN
+    if (!ctx || !cards || n_in < 1 || !in_tables || !in_ndims || !in_vars || !out_table)
+        return set_err(BNPP_ERR_INVALID, "null argument");
+    if (n_in > kMaxIn) return set_err(BNPP_ERR_UNSUPPORTED, "at most 8 inputs per fused call");
+    int max_var = elim_var;
+    for (int i = 0; i < n_in; ++i) {
+        for (int j = 0; j < in_ndims[i]; ++j) max_var = std::max(max_var, in_vars[i][j]);
+    }
+    for (int j = 0; j < out_ndims; ++j) max_var = std::max(max_var, out_vars[j]);
+    std::vector<int> cv(cards, cards + max_var + 1);
+    for (int i = 0; i < n_in; ++i)
+        if (!valid_scope(in_ndims[i], in_vars[i], cv.data(), 0)) return set_err(BNPP_ERR_INVALID, "bad input scope");
+    if (!valid_scope(out_ndims, out_vars, cv.data(), 0)) return set_err(BNPP_ERR_INVALID, "bad output scope");
+    BucketSpec b;
+    std::vector<const void *> ptrs;
+    for (int i = 0; i < n_in; ++i) {
+        std::vector<int> s(in_vars[i], in_vars[i] + in_ndims[i]);
+        b.in.push_back(natural_view(i, s, cv));
+        ptrs.push_back(in_tables[i]);
+    }
+    b.elim_var = elim_var;
+    // the output must hold exactly the kept variables (domain.cpp:32-72), in any order
+    std::vector<int> u = chain_scope(b.in);
+    if (elim_var >= 0) u = remove_var(u, elim_var);
+    std::vector<int> ov(out_vars, out_vars + out_ndims), us = u, os = ov;
+    std::sort(us.begin(), us.end());
+    std::sort(os.begin(), os.end());
+    if (us != os) return set_err(BNPP_ERR_INVALID, "output scope must be the union of the inputs minus elim_var");
+    b.out_vars = ov;
+    b.out_table = n_in;
+    return run_single(ctx, stream, dtype, cv, b, ptrs, out_table);
+    BNPP_GUARD_END
+}
+
+int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *a, int a_ndims,
+                 const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
+                 const int *out_vars) {
+    const void *tabs[2] = {a, b};
+    const int nd[2] = {a_ndims, b_ndims};
+    const int *vs[2] = {a_vars, b_vars};
+    return bnpp_bucket_eliminate(ctx, stream, dtype, cards, 2, tabs, nd, vs, -1, out, out_ndims, out_vars);
+}
+
+int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
+                 const int *vars, int var, void *out, int out_ndims, const int *out_vars) {
+    const void *tabs[1] = {in};
+    return bnpp_bucket_eliminate(ctx, stream, dtype, cards, 1, tabs, &ndims, &vars, var, out, out_ndims, out_vars);
+}
+
+int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
+                   const int *vars, int n_ev, const int *ev_vars, const int *ev_vals, void *out) {
+    BNPP_GUARD_BEGIN
+    if (!ctx || !cards || !in || !out || (ndims > 0 && !vars) || n_ev < 0 || (n_ev > 0 && (!ev_vars || !ev_vals)))
+        return set_err(BNPP_ERR_INVALID, "null argument");
+    int max_var = 0;
+    for (int j = 0; j < ndims; ++j) max_var = std::max(max_var, vars[j]);
+    std::vector<int> cv(cards, cards + max_var + 1);
+    if (!valid_scope(ndims, vars, cv.data(), 0)) return set_err(BNPP_ERR_INVALID, "bad scope");
+    std::vector<int> ev(max_var + 1, -1);
+    for (int i = 0; i < n_ev; ++i) {
+        int v = ev_vars[i];
+        if (v < 0) return set_err(BNPP_ERR_INVALID, "bad evidence variable");
+        if (v > max_var) continue;                          // not in this factor's scope
+        if (ev_vals[i] < 0 || ev_vals[i] >= cv[v]) return set_err(BNPP_ERR_INVALID, "evidence value out of range");
+        ev[v] = ev_vals[i];
+    }
+    std::vector<int> s(vars, vars + ndims);
+    BucketSpec b;
+    b.in.push_back(conditioned_view(0, s, cv, ev));
+    b.out_vars = b.in[0].vars;
+    b.out_table = 1;
+    return run_single(ctx, stream, dtype, cv, b, {in}, out);
+    BNPP_GUARD_END
+}
+
+int bnpp_model_load_uai(const char *path, bnpp_model **out) {
+    BNPP_GUARD_BEGIN
+    if (!path || !out) return set_err(BNPP_ERR_INVALID, "null argument");
+    *out = nullptr;
+    std::unique_ptr<bnpp_model> m(new bnpp_model);
+    std::string err;
+    if (load_uai(path, m->d, &err)) return set_err(BNPP_ERR_IO, err);
+    *out = m.release();
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_model_from_arrays(int is_bayes, int n_vars, const int *cards, int n_factors, const int *widths,
+                           const int *scopes, const double *values, bnpp_model **out) {
+    BNPP_GUARD_BEGIN
+    if (!out || n_vars < 0 || n_factors < 0 || (n_vars > 0 && !cards) || (n_factors > 0 && (!widths || !scopes || !values)))
+        return set_err(BNPP_ERR_INVALID, "bad arguments");
+    *out = nullptr;
+    std::unique_ptr<bnpp_model> m(new bnpp_model);
+    m->d.is_bayes = is_bayes != 0;
+    m->d.cards.assign(cards, cards + n_vars);
+    for (int c : m->d.cards)
+        if (c < 1) return set_err(BNPP_ERR_INVALID, "cardinality must be >= 1");
+    const int *sc = scopes;
+    const double *vals = values;
+    for (int f = 0; f < n_factors; ++f) {
+        if (widths[f] < 0) return set_err(BNPP_ERR_INVALID, "negative width");
+        std::vector<int> s(sc, sc + widths[f]);
+        sc += widths[f];
+        int64_t sz = 1;
+        for (int v : s) {
+            if (v < 0 || v >= n_vars) return set_err(BNPP_ERR_INVALID, "scope id out of range");
+            sz *= m->d.cards[v];
+        }
+        m->d.scopes.push_back(s);
+        m->d.values.emplace_back(vals, vals + sz);
+        vals += sz;
+    }
+    std::string err;
+    if (!validate(m->d, &err)) return set_err(BNPP_ERR_INVALID, err);
+    *out = m.release();
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_model_free(bnpp_model *m) {
+    delete m;
+    return BNPP_OK;
+}
+
+int bnpp_model_info(const bnpp_model *m, int *is_bayes, int *n_vars, int *n_factors) {
+    if (!m) return set_err(BNPP_ERR_INVALID, "null model");
+    if (is_bayes) *is_bayes = m->d.is_bayes ? 1 : 0;
+    if (n_vars) *n_vars = (int)m->d.cards.size();
+    if (n_factors) *n_factors = (int)m->d.scopes.size();
+    return BNPP_OK;
+}
+
+int bnpp_model_cards(const bnpp_model *m, int *cards) {
+    if (!m || !cards) return set_err(BNPP_ERR_INVALID, "null argument");
+    std::copy(m->d.cards.begin(), m->d.cards.end(), cards);
+    return BNPP_OK;
+}
+
+int bnpp_evidence_load(const char *path, int cap, int *n, int *vars, int *vals) {
+    BNPP_GUARD_BEGIN
+    if (!path || !n) return set_err(BNPP_ERR_INVALID, "null argument");
+    std::vector<std::pair<int, int>> ev;
+    if (load_evidence(path, ev)) return set_err(BNPP_ERR_IO, std::string("couldn't read file ") + path);
+    *n = (int)ev.size();
+    if ((int)ev.size() > cap) return set_err(BNPP_ERR_INVALID, "evidence larger than cap");
+    for (size_t i = 0; i < ev.size(); ++i) {
+        vars[i] = ev[i].first;
+        vals[i] = ev[i].second;
+    }
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_ordering(const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals, int n_vars,
+                  const int *vars, int heuristic, int *order_out, int *width_out) {
+    BNPP_GUARD_BEGIN
+    if (!m || !order_out) return set_err(BNPP_ERR_INVALID, "null argument");
+    if (heuristic < BNPP_ORDER_GIVEN || heuristic > BNPP_MIN_DEGREE) return set_err(BNPP_ERR_INVALID, "unknown heuristic");
+    const ModelData &d = m->d;
+    std::vector<int> ev;
+    std::string msg;
+    if (!evidence_array(d, n_ev, ev_vars, ev_vals, ev, msg)) return set_err(BNPP_ERR_INVALID, msg);
+    std::vector<int> vs;
+    if (vars) {
+        for (int i = 0; i < n_vars; ++i) {
+            if (vars[i] < 0 || vars[i] >= (int)d.cards.size()) return set_err(BNPP_ERR_INVALID, "bad variable");
+            vs.push_back(vars[i]);
+        }
+    } else {
+        for (int v = 0; v < (int)d.cards.size(); ++v)
+            if (ev[v] < 0) vs.push_back(v);
+    }
+    std::vector<int> ord;
+    int w = elimination_order((int)d.cards.size(), d.cards, conditioned_scopes(d, ev), vs, (Heuristic)heuristic, ord);
+    std::copy(ord.begin(), ord.end(), order_out);
+    if (width_out) *width_out = w;
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_job_create(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals,
+                    int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
+                    bnpp_job **out) {
+    BNPP_GUARD_BEGIN
+    if (!out) return set_err(BNPP_ERR_INVALID, "null output");
+    *out = nullptr;
+    if (kind != 0 && kind != 1) return set_err(BNPP_ERR_INVALID, "kind must be 0 (partition) or 1 (marginals)");
+    std::unique_ptr<bnpp_job> job;
+    int rc = create_job(ctx, m, kind, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job);
+    if (rc) {
+        if (job) destroy_job(job.release());
+        return rc;
+    }
+    *out = job.release();
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_variable_elimination(bnpp_ctx *ctx, const bnpp_model *m, int n_vars, const int *vars, int heuristic,
+                              int dtype, int cap_vars, int *out_ndims, int *out_vars, int64_t cap_values,
+                              int64_t *out_size, double *out_values, int64_t *exp2) {
+    BNPP_GUARD_BEGIN
+    if (!out_ndims || !out_size || !exp2 || (n_vars > 0 && !vars)) return set_err(BNPP_ERR_INVALID, "null argument");
+    std::unique_ptr<bnpp_job> job;
+    int rc = create_job(ctx, m, 2, 0, nullptr, nullptr, heuristic, vars, n_vars, 0, nullptr, dtype, job);
+    if (rc == BNPP_OK) rc = from_ctx(ctx, launch(ctx->c, job->ex, ctx->c.stream));
+    std::vector<std::vector<double>> vals;
+    std::vector<int64_t> e2;
+    if (rc == BNPP_OK) rc = from_ctx(ctx, fetch_results(ctx->c, job->ex, ctx->c.stream, vals, e2));
+    if (rc == BNPP_OK) {
+        const std::vector<int> &rv = job->ex.sched.plan_result_vars[0];
+        *out_ndims = (int)rv.size();
+        *out_size = (int64_t)vals[0].size();
+        *exp2 = e2[0];
+        if ((int)rv.size() > cap_vars || (int64_t)vals[0].size() > cap_values) {
+            rc = set_err(BNPP_ERR_INVALID, "result larger than the output capacity");
+        } else {
+            std::copy(rv.begin(), rv.end(), out_vars);
+            std::copy(vals[0].begin(), vals[0].end(), out_values);
+        }
+    }
+    if (job) destroy_job(job.release());
+    return rc;
+    BNPP_GUARD_END
+}
+
+int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
+                    int dtype, double *stats, int n_stats) {
+    BNPP_GUARD_BEGIN
+    if (!m || !stats) return set_err(BNPP_ERR_INVALID, "null argument");
+    if (kind != 0 && kind != 1) return set_err(BNPP_ERR_INVALID, "kind must be 0 or 1");
+    std::vector<int> ev, targets;
+    std::string msg;
+    if (!evidence_array(m->d, n_ev, ev_vars, ev_vals, ev, msg)) return set_err(BNPP_ERR_INVALID, msg);
+    if (kind == 1)
+        for (int v = 0; v < (int)m->d.cards.size(); ++v) targets.push_back(v);
+    Schedule s;
+    double st[8] = {0};
+    int rc = plan_schedule(m->d, ev, kind, heuristic, nullptr, 0, targets, dtype, s, st);
+    if (rc) return rc;
+    for (int i = 0; i < n_stats && i < 8; ++i) stats[i] = st[i];
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_job_stats(const bnpp_job *job, double *stats, int n_stats) {
+    if (!job || !stats) return set_err(BNPP_ERR_INVALID, "null argument");
+    for (int i = 0; i < n_stats && i < 8; ++i) stats[i] = job->stats[i];
+    return BNPP_OK;
+}
+
+int bnpp_job_launch(bnpp_job *job, void *stream) {
+    BNPP_GUARD_BEGIN
+    if (!job) return set_err(BNPP_ERR_INVALID, "null job");
+    (void)hipSetDevice(job->ctx->c.device);
+    return from_ctx(job->ctx, launch(job->ctx->c, job->ex, pick_stream(job->ctx, stream)));
+    BNPP_GUARD_END
+}
+
+int bnpp_job_results(bnpp_job *job, void *stream, double *out) {
+    BNPP_GUARD_BEGIN
+    if (!job || !out) return set_err(BNPP_ERR_INVALID, "null argument");
+    (void)hipSetDevice(job->ctx->c.device);
+    return job_results(job, pick_stream(job->ctx, stream), out, nullptr);
+    BNPP_GUARD_END
+}
+
+int bnpp_job_free(bnpp_job *job) {
+    destroy_job(job);
+    return BNPP_OK;
+}
+
+int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                   int heuristic, const int *order, int n_order, int dtype, double *log10_z, double *z,
+                   double *uptime_ms) {
+    BNPP_GUARD_BEGIN
+    double t0 = now_ms();
+    std::unique_ptr<bnpp_job> job;
+    int rc = create_job(ctx, m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype, job);
+    if (rc == BNPP_OK) rc = from_ctx(ctx, launch(ctx->c, job->ex, ctx->c.stream));
+    double lz = 0, zz = 0;
+    if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, &lz, &zz);
+    if (job) destroy_job(job.release());
+    if (rc) return rc;
+    if (log10_z) *log10_z = lz;
+    if (z) *z = zz;
+    if (uptime_ms) *uptime_ms = now_ms() - t0;
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                   int heuristic, int n_targets, const int *targets, int dtype, double *out, double *uptime_ms) {
+    BNPP_GUARD_BEGIN
+    if (!out) return set_err(BNPP_ERR_INVALID, "null output");
+    double t0 = now_ms();
+    std::unique_ptr<bnpp_job> job;
+    int rc = create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, job);
+    if (rc == BNPP_OK) rc = from_ctx(ctx, launch(ctx->c, job->ex, ctx->c.stream));
+    if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
+    if (job) destroy_job(job.release());
+    if (rc) return rc;
+    if (uptime_ms) *uptime_ms = now_ms() - t0;
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+}  // extern "C"

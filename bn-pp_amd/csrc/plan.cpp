@@ -1,0 +1,435 @@
+// Host-side planning: scope rules, descriptor compilation, symbolic VE, schedule.
+#include "plan.hpp"
+
+#include <algorithm>
+#include <climits>
+#include <map>
+
+namespace bnpp {
+
+std::vector<int64_t> natural_strides(const std::vector<int> &vars, const std::vector<int> &cards) {
+    std::vector<int64_t> s(vars.size());
+    int64_t acc = 1;
+    for (int i = (int)vars.size() - 1; i >= 0; --i) {
+        s[i] = acc;
+        acc *= cards[vars[i]];
+    }
+    return s;
+}
+
+int64_t table_size(const std::vector<int> &vars, const std::vector<int> &cards) {
+    int64_t s = 1;
+    for (int v : vars) s *= cards[v];
+    return s;
+}
+
+View natural_view(int table, const std::vector<int> &vars, const std::vector<int> &cards) {
+    View v;
+    v.table = table;
+    v.vars = vars;
+    v.strides = natural_strides(vars, cards);
+    return v;
+}
+
+View conditioned_view(int table, const std::vector<int> &vars, const std::vector<int> &cards,
+                      const std::vector<int> &ev_val) {
+    std::vector<int64_t> st = natural_strides(vars, cards);
+    View v;
+    v.table = table;
+    for (size_t i = 0; i < vars.size(); ++i) {
+        int e = vars[i] < (int)ev_val.size() ? ev_val[vars[i]] : -1;
+        if (e >= 0) {
+            v.base += (int64_t)e * st[i];
+        } else {
+            v.vars.push_back(vars[i]);
+            v.strides.push_back(st[i]);
+        }
+    }
+    return v;
+}
+
+static bool contains(const std::vector<int> &s, int v) { return std::find(s.begin(), s.end(), v) != s.end(); }
+
+std::vector<int> union_scope(const std::vector<int> &a, const std::vector<int> &b) {
+    std::vector<int> u = a;
+    for (int v : b)
+        if (!contains(a, v)) u.push_back(v);
+    return u;
+}
+
+std::vector<int> chain_scope(const std::vector<View> &in) {
+    std::vector<int> u;                      // Factor(1.0) has the empty scope
+    for (const View &v : in) u = union_scope(u, v.vars);
+    return u;
+}
+
+std::vector<int> remove_var(const std::vector<int> &s, int v) {
+    std::vector<int> r;
+    for (int x : s)
+        if (x != v) r.push_back(x);
+    return r;
+}
+
+namespace {
+struct Dim {
+    uint64_t card;
+    int64_t s[kMaxIn];
+};
+
+void magic_for(uint32_t d, uint32_t &shift, uint32_t &magic, bool &pow2) {
+    pow2 = (d & (d - 1)) == 0;
+    uint32_t l = 0;
+    while (((uint64_t)1 << l) < d) ++l;
+    shift = l;
+    if (pow2) {
+        magic = 0;
+    } else {
+        magic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+    }
+}
+}  // namespace
+
+bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec, BucketDesc &d,
+                std::vector<int64_t> &pool, std::string *msg) {
+    const int n = (int)b.in.size();
+    if (n < 1 || n > kMaxIn) {
+        if (msg) *msg = "bucket needs 1.." + std::to_string(kMaxIn) + " inputs, got " + std::to_string(n);
+        return false;
+    }
+    if (b.elim_var >= 0 && contains(b.out_vars, b.elim_var)) {
+        if (msg) *msg = "summed variable appears in the output scope";
+        return false;
+    }
+    for (const View &v : b.in) {
+        if (v.vars.size() != v.strides.size()) {
+            if (msg) *msg = "view vars/strides length mismatch";
+            return false;
+        }
+        for (int x : v.vars)
+            if (x != b.elim_var && !contains(b.out_vars, x)) {
+                if (msg) *msg = "input variable " + std::to_string(x) + " is neither kept nor summed";
+                return false;
+            }
+    }
+    std::vector<Dim> dims;    // slowest first
+    int64_t out_size = 1;
+    for (int u : b.out_vars) {
+        int c = cards[u];
+        if (c < 1) {
+            if (msg) *msg = "cardinality must be >= 1";
+            return false;
+        }
+        out_size *= c;
+        if (c == 1) continue;
+        Dim dm;
+        dm.card = (uint64_t)c;
+        for (int i = 0; i < kMaxIn; ++i) dm.s[i] = 0;
+        for (int i = 0; i < n; ++i)
+            for (size_t j = 0; j < b.in[i].vars.size(); ++j)
+                if (b.in[i].vars[j] == u) dm.s[i] = b.in[i].strides[j];
+        dims.push_back(dm);
+    }
+    // merge adjacent dims that are contiguous in every input (fastest first)
+    std::vector<Dim> merged;
+    for (int j = (int)dims.size() - 1; j >= 0; --j) {
+        const Dim &dm = dims[j];
+        bool ok = !merged.empty();
+        if (ok) {
+            Dim &bk = merged.back();
+            if (bk.card * dm.card > (uint64_t)INT32_MAX) ok = false;
+            for (int i = 0; ok && i < n; ++i)
+                if (dm.s[i] != bk.s[i] * (int64_t)bk.card) ok = false;
+            if (ok) bk.card *= dm.card;
+        }
+        if (!ok) merged.push_back(dm);
+    }
+    int k = 1;
+    int64_t es[kMaxIn] = {0};
+    if (b.elim_var >= 0) {
+        for (int i = 0; i < n; ++i)
+            for (size_t j = 0; j < b.in[i].vars.size(); ++j)
+                if (b.in[i].vars[j] == b.elim_var) {
+                    es[i] = b.in[i].strides[j];
+                    k = cards[b.elim_var];
+                }
+    }
+    // widest vector that divides the fastest dim and keeps stride-1 inputs aligned
+    int vec = 1;
+    if (!merged.empty()) {
+        for (int v = max_vec; v >= 2; v >>= 1) {
+            if (merged[0].card % (uint64_t)v) continue;
+            bool ok = true;
+            for (int i = 0; ok && i < n; ++i) {
+                if (merged[0].s[i] != 1) continue;
+                if (b.in[i].base % v || es[i] % v) ok = false;
+                for (size_t j = 1; ok && j < merged.size(); ++j)
+                    if (merged[j].s[i] % v) ok = false;
+            }
+            if (ok) { vec = v; break; }
+        }
+    }
+    d = BucketDesc{};
+    d.out_size = out_size;
+    d.vec = vec;
+    d.n_vec = out_size / vec;
+    d.n_in = n;
+    d.n_dims = (int)merged.size();
+    d.k = k;
+    d.out_table = b.out_table;
+    d.flags = kScale | kTrackMax;
+    for (int i = 0; i < kMaxIn; ++i) {
+        d.in_table[i] = i < n ? b.in[i].table : 0;
+        d.in_base[i] = i < n ? b.in[i].base : 0;
+        d.elim_stride[i] = es[i];
+    }
+    d.dim_off = (int64_t)pool.size();
+    for (const Dim &dm : merged) {
+        uint32_t shift, magic;
+        bool pow2;
+        magic_for((uint32_t)dm.card, shift, magic, pow2);
+        pool.push_back(pack_dim_header((uint32_t)dm.card, shift, pow2));
+        pool.push_back((int64_t)magic);
+        for (int i = 0; i < n; ++i) pool.push_back(dm.s[i]);
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- VE plan
+VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, const std::vector<int> &order,
+               bool canonical) {
+    VEPlan p;
+    p.n_src = (int)sources.size();
+    const int nv = (int)cards.size();
+    std::vector<int> rank(nv, -1);
+    for (int i = (int)order.size() - 1; i >= 0; --i) rank[order[i]] = i;
+
+    // layout key: earlier-eliminated variables are slower; kept variables last
+    auto canon = [&](std::vector<int> s) {
+        if (!canonical) return s;
+        std::stable_sort(s.begin(), s.end(), [&](int a, int b) {
+            int64_t ka = rank[a] >= 0 ? rank[a] : (int64_t)nv + a;
+            int64_t kb = rank[b] >= 0 ? rank[b] : (int64_t)nv + b;
+            return ka < kb;
+        });
+        return s;
+    };
+    std::vector<int> level(p.n_src, 0);     // per table
+    auto new_msg = [&](const std::vector<int> &vars) {
+        MsgTable t;
+        t.vars = vars;
+        t.size = table_size(vars, cards);
+        p.max_table = std::max(p.max_table, t.size);
+        p.msgs.push_back(t);
+        level.push_back(0);
+        return p.n_src + (int)p.msgs.size() - 1;
+    };
+    auto table_view = [&](int id) { return natural_view(id, p.msgs[id - p.n_src].vars, cards); };
+    auto entries_of = [&](const std::vector<View> &in) {
+        double e = 1;
+        for (int v : chain_scope(in)) e *= cards[v];
+        return e;
+    };
+    auto moved_of = [&](const std::vector<View> &in, int out_table) {
+        double e = (double)p.msgs[out_table - p.n_src].size;
+        for (const View &v : in) e += (double)table_size(v.vars, cards);
+        return e;
+    };
+    // emit a bucket over `in` (any length) summing out `x` (-1: none) into a table laid out as `layout(vars)`
+    auto emit = [&](std::vector<View> in, int x, bool final_result) -> int {
+        while ((int)in.size() > kMaxIn) {
+            std::vector<View> head(in.begin(), in.begin() + kMaxIn);
+            std::vector<int> hv = canon(chain_scope(head));
+            BucketSpec b;
+            b.in = head;
+            b.out_vars = hv;
+            b.out_table = new_msg(hv);
+            int lv = 0;
+            for (const View &v : head) lv = std::max(lv, level[v.table]);
+            b.level = lv + 1;
+            level[b.out_table] = b.level;
+            p.entries += entries_of(head);
+            p.elems_moved += moved_of(head, b.out_table);
+            std::vector<View> rest;
+            rest.push_back(table_view(b.out_table));
+            rest.insert(rest.end(), in.begin() + kMaxIn, in.end());
+            p.buckets.push_back(b);
+            in.swap(rest);
+        }
+        std::vector<int> u = chain_scope(in);
+        std::vector<int> ov = x >= 0 ? remove_var(u, x) : u;
+        if (!final_result) ov = canon(ov);
+        BucketSpec b;
+        b.in = in;
+        b.elim_var = x;
+        b.out_vars = ov;
+        b.out_table = new_msg(ov);
+        int lv = 0;
+        for (const View &v : in) lv = std::max(lv, level[v.table]);
+        b.level = lv + 1;
+        level[b.out_table] = b.level;
+        p.entries += entries_of(in);
+        p.elems_moved += moved_of(in, b.out_table);
+        p.width = std::max(p.width, (int)ov.size());
+        p.buckets.push_back(b);
+        return b.out_table;
+    };
+
+    const int nord = (int)order.size();
+    std::vector<std::vector<View>> buckets(nord);
+    std::vector<View> result;
+    auto first_bucket = [&](const std::vector<int> &vars, int from) {
+        int best = -1;
+        for (int v : vars) {
+            int r = v < nv ? rank[v] : -1;
+            if (r >= from && (best < 0 || r < best)) best = r;
+        }
+        return best;
+    };
+    for (const View &s : sources) {                                   // model.cpp:394-406
+        int bi = first_bucket(s.vars, 0);
+        if (bi >= 0) buckets[bi].push_back(s);
+        else result.push_back(s);
+    }
+    for (int i = 0; i < nord; ++i) {                                  // model.cpp:409-439
+        if (buckets[i].empty()) continue;   // Factor(1.0).sum_out(x) == 1: result *= 1 is exact
+        int t = emit(buckets[i], order[i], false);
+        View mv = table_view(t);
+        int bi = first_bucket(mv.vars, i + 1);
+        if (bi >= 0) buckets[bi].push_back(mv);
+        else result.push_back(mv);
+    }
+    if (!result.empty()) {
+        p.result_table = emit(result, -1, true);
+        p.result_vars = p.msgs[p.result_table - p.n_src].vars;
+    }
+    // order buckets by level (stable), levels are 1-based
+    std::stable_sort(p.buckets.begin(), p.buckets.end(),
+                     [](const BucketSpec &a, const BucketSpec &b) { return a.level < b.level; });
+    p.n_levels = p.buckets.empty() ? 0 : p.buckets.back().level;
+    return p;
+}
+
+// ------------------------------------------------------------- schedule
+namespace {
+struct Arena {
+    std::map<int64_t, int64_t> free_;   // offset -> length
+    int64_t top = 0;
+    int64_t alloc(int64_t n) {
+        n = (n + 255) & ~(int64_t)255;
+        for (auto it = free_.begin(); it != free_.end(); ++it) {
+            if (it->second >= n) {
+                int64_t off = it->first, len = it->second;
+                free_.erase(it);
+                if (len > n) free_[off + n] = len - n;
+                return off;
+            }
+        }
+        // extend: merge with a trailing free block if present
+        if (!free_.empty()) {
+            auto last = std::prev(free_.end());
+            if (last->first + last->second == top) {
+                int64_t off = last->first;
+                free_.erase(last);
+                top = off + n;
+                return off;
+            }
+        }
+        int64_t off = top;
+        top += n;
+        return off;
+    }
+    void release(int64_t off, int64_t n) {
+        n = (n + 255) & ~(int64_t)255;
+        auto it = free_.emplace(off, n).first;
+        auto nx = std::next(it);
+        if (nx != free_.end() && it->first + it->second == nx->first) {
+            it->second += nx->second;
+            free_.erase(nx);
+        }
+        if (it != free_.begin()) {
+            auto pv = std::prev(it);
+            if (pv->first + pv->second == it->first) {
+                pv->second += it->second;
+                free_.erase(it);
+            }
+        }
+    }
+};
+}  // namespace
+
+bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<int> &cards,
+                    const std::vector<int64_t> &src_sizes, int elem_bytes, int max_vec, Schedule &s,
+                    std::string *msg) {
+    s = Schedule{};
+    s.n_src = (int)src_sizes.size();
+    s.table_size = src_sizes;
+    s.table_offset.assign(src_sizes.size(), -1);
+    std::vector<int> msg_base;
+    int n_levels = 0;
+    for (const VEPlan *p : plans) {
+        if (p->n_src != s.n_src) {
+            if (msg) *msg = "plans disagree on the number of sources";
+            return false;
+        }
+        msg_base.push_back((int)s.table_size.size());
+        for (const MsgTable &t : p->msgs) s.table_size.push_back(t.size);
+        n_levels = std::max(n_levels, p->n_levels);
+        s.entries += p->entries;
+        s.elems_moved += p->elems_moved;
+        s.width = std::max(s.width, p->width);
+    }
+    s.n_tables = (int)s.table_size.size();
+    s.table_offset.resize(s.n_tables, -1);
+    auto remap = [&](size_t pi, int t) { return t < s.n_src ? t : msg_base[pi] + (t - s.n_src); };
+
+    // lifetimes: produced level, last consuming level
+    const int kForever = INT_MAX;
+    std::vector<int> born(s.n_tables, 0), last(s.n_tables, -1);
+    for (size_t pi = 0; pi < plans.size(); ++pi) {
+        for (const BucketSpec &b : plans[pi]->buckets) {
+            born[remap(pi, b.out_table)] = b.level;
+            for (const View &v : b.in) {
+                int t = remap(pi, v.table);
+                last[t] = std::max(last[t], b.level);
+            }
+        }
+        if (plans[pi]->result_table >= 0) last[remap(pi, plans[pi]->result_table)] = kForever;
+        s.plan_result_table.push_back(plans[pi]->result_table >= 0 ? remap(pi, plans[pi]->result_table) : -1);
+        s.plan_result_vars.push_back(plans[pi]->result_vars);
+    }
+    std::vector<std::vector<int>> born_at(n_levels + 2), dies_at(n_levels + 2);
+    for (int t = s.n_src; t < s.n_tables; ++t) {
+        born_at[born[t]].push_back(t);
+        if (last[t] != kForever) dies_at[std::max(last[t], born[t])].push_back(t);
+    }
+    Arena arena;
+    for (int L = 1; L <= n_levels; ++L) {
+        for (int t : born_at[L]) s.table_offset[t] = arena.alloc(s.table_size[t] * elem_bytes);
+        for (int t : dies_at[L]) arena.release(s.table_offset[t], s.table_size[t] * elem_bytes);
+    }
+    s.arena_bytes = arena.top;
+
+    // descriptors, level by level
+    std::vector<std::vector<std::pair<size_t, const BucketSpec *>>> by_level(n_levels + 1);
+    for (size_t pi = 0; pi < plans.size(); ++pi)
+        for (const BucketSpec &b : plans[pi]->buckets) by_level[b.level].push_back({pi, &b});
+    for (int L = 1; L <= n_levels; ++L) {
+        s.level_begin.push_back((int)s.descs.size());
+        int64_t vb = 0;
+        for (auto &pb : by_level[L]) {
+            BucketSpec b = *pb.second;
+            for (View &v : b.in) v.table = remap(pb.first, v.table);
+            b.out_table = remap(pb.first, b.out_table);
+            BucketDesc d;
+            if (!build_desc(b, cards, max_vec, d, s.pool, msg)) return false;
+            d.vblk_begin = vb;
+            vb += (d.n_vec + kBlock - 1) / kBlock;
+            s.descs.push_back(d);
+        }
+        s.level_vblocks.push_back(vb);
+    }
+    s.level_begin.push_back((int)s.descs.size());
+    return true;
+}
+
+}  // namespace bnpp

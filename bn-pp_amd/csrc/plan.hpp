@@ -1,0 +1,97 @@
+// Host-side planning for the fused bucket kernels (no HIP calls; unit-testable on CPU).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "bnpp_device.h"
+
+namespace bnpp {
+
+// A table as one bucket input sees it: table id, evidence base offset, and the
+// (variable, stride) pairs that remain after conditioning (domain.cpp:74-90).
+struct View {
+    int table = -1;
+    int64_t base = 0;
+    std::vector<int> vars;
+    std::vector<int64_t> strides;
+};
+
+// Row-major strides, last variable fastest (domain.cpp:15-26).
+std::vector<int64_t> natural_strides(const std::vector<int> &vars, const std::vector<int> &cards);
+int64_t table_size(const std::vector<int> &vars, const std::vector<int> &cards);
+View natural_view(int table, const std::vector<int> &vars, const std::vector<int> &cards);
+// Factor::conditioning as a view (factor.cpp:214-242): evidence vars leave the
+// scope and move into the base offset.  ev_val[v] < 0 means "no evidence on v".
+View conditioned_view(int table, const std::vector<int> &vars, const std::vector<int> &cards,
+                      const std::vector<int> &ev_val);
+
+// Scope rules of the reference.
+std::vector<int> union_scope(const std::vector<int> &a, const std::vector<int> &b);   // domain.cpp:32-41
+std::vector<int> chain_scope(const std::vector<View> &in);                             // Factor(1.0) *= ...
+std::vector<int> remove_var(const std::vector<int> &s, int v);                         // domain.cpp:54-59
+
+struct BucketSpec {
+    std::vector<View> in;
+    int elim_var = -1;              // -1: pure product
+    std::vector<int> out_vars;      // output layout (slowest first)
+    int out_table = -1;
+    int level = 0;
+};
+
+// Compile one bucket into a descriptor + dims-pool rows.  max_vec: 4 (fp32) / 2 (fp64).
+// Returns false (with msg) on an invalid shape.
+bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec, BucketDesc &d,
+                std::vector<int64_t> &pool, std::string *msg);
+
+struct MsgTable {
+    std::vector<int> vars;
+    int64_t size = 1;
+};
+
+// Symbolic VE plan (BN::variable_elimination, model.cpp:348-446).
+struct VEPlan {
+    int n_src = 0;                      // tables [0, n_src) are the (conditioned) sources
+    std::vector<MsgTable> msgs;         // table id = n_src + index
+    std::vector<BucketSpec> buckets;    // execution order (non-decreasing level)
+    int n_levels = 0;
+    int result_table = -1;              // -1: result is the constant 1 (no factors)
+    std::vector<int> result_vars;
+    int64_t max_table = 0;              // largest message entries
+    double entries = 0;                 // sum over buckets of prod(card) over the union scope
+    double elems_moved = 0;             // sum over buckets of (|inputs| + |output|): algorithmic traffic
+    int width = 0;                      // largest bucket output width
+};
+
+// canonical: lay messages out with variables sorted by elimination rank
+// (earlier-eliminated slower) instead of the reference's chain order; values
+// are identical, only the storage permutation differs.  Buckets with more than
+// kMaxIn inputs are split into materialised pure-product prefixes exactly like
+// the reference's left-to-right chain.
+VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, const std::vector<int> &order,
+               bool canonical);
+
+// Flattened, level-ordered launch schedule over one or more plans sharing the
+// same sources.  Tables: [0, n_src) sources, then every plan's messages.
+struct Schedule {
+    int n_src = 0;
+    int n_tables = 0;
+    std::vector<int64_t> table_size;        // entries, per table (sources included)
+    std::vector<int64_t> table_offset;      // bytes into the arena (messages only; -1 for sources)
+    std::vector<BucketDesc> descs;          // grouped by level, vblk_begin relative to the level
+    std::vector<int64_t> pool;
+    std::vector<int> level_begin;           // descs index where each level starts (+ end sentinel)
+    std::vector<int64_t> level_vblocks;     // virtual blocks per level
+    std::vector<int> plan_result_table;     // per plan (-1: constant 1)
+    std::vector<std::vector<int>> plan_result_vars;
+    int64_t arena_bytes = 0;
+    double entries = 0;
+    double elems_moved = 0;
+    int width = 0;
+};
+
+bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<int> &cards,
+                    const std::vector<int64_t> &src_sizes, int elem_bytes, int max_vec, Schedule &s,
+                    std::string *msg);
+
+}  // namespace bnpp

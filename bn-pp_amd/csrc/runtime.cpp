@@ -1,0 +1,179 @@
+// Device runtime: source upload, executable schedules, launches, result fetch.
+#include "runtime.hpp"
+
+#include <cmath>
+#include <cstring>
+
+namespace bnpp {
+namespace {
+
+int fail(Context &ctx, hipError_t e, const char *what) {
+    ctx.last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return e == hipErrorOutOfMemory ? -3 : -4;
+}
+
+template <typename T>
+uint64_t bits_of(T x) {
+    uint64_t b = 0;
+    std::memcpy(&b, &x, sizeof(T));
+    return b;
+}
+
+}  // namespace
+
+int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out) {
+    const size_t eb = dt == kF32 ? 4 : 8;
+    out = DeviceSources{};
+    out.dtype = dt;
+    std::vector<size_t> off(values.size());
+    size_t total = 0;
+    for (size_t f = 0; f < values.size(); ++f) {
+        off[f] = total;
+        total += ((values[f].size() * eb + 255) / 256) * 256;
+    }
+    std::vector<unsigned char> host(total ? total : 256, 0);
+    out.meta.resize(values.size());
+    out.size.resize(values.size());
+    for (size_t f = 0; f < values.size(); ++f) {
+        double mx = 0;
+        for (double v : values[f]) mx = v > mx ? v : mx;
+        int e = 0;
+        if (mx > 0) std::frexp(mx, &e);            // mx = m * 2^e, m in [0.5, 1)
+        double smax = 0;
+        float fmax = 0;
+        for (size_t j = 0; j < values[f].size(); ++j) {
+            double s = std::ldexp(values[f][j], -e);   // exact power-of-two rescale
+            if (dt == kF32) {
+                float x = (float)s;
+                std::memcpy(host.data() + off[f] + j * 4, &x, 4);
+                fmax = x > fmax ? x : fmax;
+            } else {
+                std::memcpy(host.data() + off[f] + j * 8, &s, 8);
+                smax = s > smax ? s : smax;
+            }
+        }
+        out.meta[f].maxbits = dt == kF32 ? bits_of(fmax) : bits_of(smax);
+        out.meta[f].exp2 = e;
+        out.meta[f].size = (int64_t)values[f].size();
+        out.size[f] = (int64_t)values[f].size();
+    }
+    hipError_t err = hipSetDevice(ctx.device);
+    if (err != hipSuccess) return fail(ctx, err, "hipSetDevice");
+    err = hipMalloc(&out.buf, host.size());
+    if (err != hipSuccess) return fail(ctx, err, "hipMalloc(sources)");
+    err = hipMemcpy(out.buf, host.data(), host.size(), hipMemcpyHostToDevice);
+    if (err != hipSuccess) return fail(ctx, err, "hipMemcpy(sources)");
+    for (size_t f = 0; f < values.size(); ++f) out.meta[f].ptr = static_cast<unsigned char *>(out.buf) + off[f];
+    return 0;
+}
+
+void free_sources(DeviceSources &s) {
+    if (s.buf) (void)hipFree(s.buf);
+    s = DeviceSources{};
+}
+
+int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex) {
+    ex = Executable{};
+    ex.dtype = src.dtype;
+    ex.sched = std::move(s);
+    Schedule &sc = ex.sched;
+    hipError_t err = hipSetDevice(ctx.device);
+    if (err != hipSuccess) return fail(ctx, err, "hipSetDevice");
+    if (sc.n_src != (int)src.meta.size()) {
+        ctx.last_error = "schedule/source count mismatch";
+        return -1;
+    }
+    err = hipMalloc(&ex.arena, sc.arena_bytes > 0 ? (size_t)sc.arena_bytes : 256);
+    if (err != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
+    ex.h_meta.resize(sc.n_tables);
+    for (int t = 0; t < sc.n_tables; ++t) {
+        if (t < sc.n_src) {
+            ex.h_meta[t] = src.meta[t];
+        } else {
+            TableMeta m{};
+            m.ptr = static_cast<unsigned char *>(ex.arena) + sc.table_offset[t];
+            m.maxbits = 0;
+            m.exp2 = 0;
+            m.size = sc.table_size[t];
+            ex.h_meta[t] = m;
+        }
+    }
+    const size_t mb = sizeof(TableMeta) * (size_t)sc.n_tables;
+    if ((err = hipMalloc(&ex.d_meta, mb + 16)) != hipSuccess) return fail(ctx, err, "hipMalloc(meta)");
+    if ((err = hipMalloc(&ex.d_meta0, mb + 16)) != hipSuccess) return fail(ctx, err, "hipMalloc(meta0)");
+    if ((err = hipMalloc(&ex.d_desc, sizeof(BucketDesc) * sc.descs.size() + 16)) != hipSuccess)
+        return fail(ctx, err, "hipMalloc(desc)");
+    if ((err = hipMalloc(&ex.d_pool, sizeof(int64_t) * sc.pool.size() + 16)) != hipSuccess)
+        return fail(ctx, err, "hipMalloc(pool)");
+    if (mb && (err = hipMemcpy(ex.d_meta0, ex.h_meta.data(), mb, hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(ctx, err, "hipMemcpy(meta)");
+    if (!sc.descs.empty() && (err = hipMemcpy(ex.d_desc, sc.descs.data(), sizeof(BucketDesc) * sc.descs.size(),
+                                              hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(ctx, err, "hipMemcpy(desc)");
+    if (!sc.pool.empty() && (err = hipMemcpy(ex.d_pool, sc.pool.data(), sizeof(int64_t) * sc.pool.size(),
+                                             hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(ctx, err, "hipMemcpy(pool)");
+    return 0;
+}
+
+int launch(Context &ctx, Executable &ex, hipStream_t stream) {
+    const Schedule &sc = ex.sched;
+    hipError_t err = hipMemcpyAsync(ex.d_meta, ex.d_meta0, sizeof(TableMeta) * (size_t)sc.n_tables,
+                                    hipMemcpyDeviceToDevice, stream);
+    if (err != hipSuccess) return fail(ctx, err, "hipMemcpyAsync(meta reset)");
+    const int n_levels = (int)sc.level_vblocks.size();
+    for (int L = 0; L < n_levels; ++L) {
+        int b0 = sc.level_begin[L], b1 = sc.level_begin[L + 1];
+        err = launch_level(ex.dtype == kF32, ex.d_desc + b0, b1 - b0, ex.d_pool, ex.d_meta, sc.level_vblocks[L],
+                           ctx.max_grid, stream);
+        if (err != hipSuccess) return fail(ctx, err, "launch_level");
+    }
+    return 0;
+}
+
+int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<std::vector<double>> &vals,
+                  std::vector<int64_t> &exp2) {
+    hipError_t err = hipStreamSynchronize(stream);
+    if (err != hipSuccess) return fail(ctx, err, "hipStreamSynchronize");
+    const Schedule &sc = ex.sched;
+    const size_t np = sc.plan_result_table.size();
+    vals.assign(np, {});
+    exp2.assign(np, 0);
+    const size_t eb = ex.dtype == kF32 ? 4 : 8;
+    for (size_t p = 0; p < np; ++p) {
+        int t = sc.plan_result_table[p];
+        if (t < 0) {                         // no factors at all: Factor(1.0)
+            vals[p] = {1.0};
+            continue;
+        }
+        TableMeta m;
+        err = hipMemcpy(&m, ex.d_meta + t, sizeof(TableMeta), hipMemcpyDeviceToHost);
+        if (err != hipSuccess) return fail(ctx, err, "hipMemcpy(meta)");
+        exp2[p] = m.exp2;
+        std::vector<unsigned char> raw((size_t)sc.table_size[t] * eb);
+        err = hipMemcpy(raw.data(), m.ptr, raw.size(), hipMemcpyDeviceToHost);
+        if (err != hipSuccess) return fail(ctx, err, "hipMemcpy(result)");
+        vals[p].resize((size_t)sc.table_size[t]);
+        for (size_t j = 0; j < vals[p].size(); ++j) {
+            if (eb == 4) {
+                float x;
+                std::memcpy(&x, raw.data() + j * 4, 4);
+                vals[p][j] = x;
+            } else {
+                std::memcpy(&vals[p][j], raw.data() + j * 8, 8);
+            }
+        }
+    }
+    return 0;
+}
+
+void free_executable(Executable &ex) {
+    if (ex.arena) (void)hipFree(ex.arena);
+    if (ex.d_meta) (void)hipFree(ex.d_meta);
+    if (ex.d_meta0) (void)hipFree(ex.d_meta0);
+    if (ex.d_desc) (void)hipFree(ex.d_desc);
+    if (ex.d_pool) (void)hipFree(ex.d_pool);
+    ex = Executable{};
+}
+
+}  // namespace bnpp

@@ -1,0 +1,67 @@
+// Device runtime: context, source upload, schedule execution (HIP).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "bnpp_device.h"
+#include "model_io.hpp"
+#include "plan.hpp"
+
+namespace bnpp {
+
+hipError_t launch_level(int is_f32, const BucketDesc *descs, int n_desc, const int64_t *pool, TableMeta *meta,
+                        int64_t total_vblocks, int max_grid, hipStream_t stream);
+
+// single bucket with the descriptor passed by value (no device-side metadata,
+// no rescaling): the exact Factor::product / sum_out / conditioning semantics.
+constexpr int kMaxPool = 320;   // dims-pool words that fit the kernel-argument segment
+struct SingleArgs {
+    BucketDesc d;
+    TableMeta meta[kMaxIn + 1];  // inputs 0..n_in-1, output at index n_in
+    int64_t pool[kMaxPool];
+};
+hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream);
+
+enum DType { kF64 = 0, kF32 = 1 };
+
+struct Context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int max_grid = 2048;
+    std::string last_error;
+};
+
+// Sources uploaded for one dtype: one device buffer, each factor pre-scaled by
+// an exact power of two so its max lies in [0.5, 1).
+struct DeviceSources {
+    DType dtype = kF64;
+    void *buf = nullptr;
+    std::vector<TableMeta> meta;
+    std::vector<int64_t> size;
+};
+
+// A schedule bound to device buffers, launchable many times.
+struct Executable {
+    DType dtype = kF64;
+    Schedule sched;
+    void *arena = nullptr;
+    TableMeta *d_meta = nullptr;        // live metadata
+    TableMeta *d_meta0 = nullptr;       // pristine copy, restored before every launch
+    BucketDesc *d_desc = nullptr;
+    int64_t *d_pool = nullptr;
+    std::vector<TableMeta> h_meta;
+};
+
+int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out);
+void free_sources(DeviceSources &s);
+int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex);
+int launch(Context &ctx, Executable &ex, hipStream_t stream);
+// waits for `stream`, downloads result tables: values as stored (double) and the exp2 scale
+int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<std::vector<double>> &vals,
+                  std::vector<int64_t> &exp2);
+void free_executable(Executable &ex);
+
+}  // namespace bnpp

@@ -1,0 +1,179 @@
+/*
+ * bnpp.h — C ABI of the MI355X-native bn-pp variable-elimination engine.
+ *
+ * The reference (GEO-IASS/bn-pp) has no FFI: its hot path sits behind the C++
+ * class API of code/factor.hh and code/model.hh.  Every entry point below names
+ * the reference interface it replaces (file:line into the reference's code/).
+ * The C++ mirror of that class API (bn::Variable/Domain/Factor/BN/MN) lives in
+ * include/bnpp/bn.hpp and is implemented on top of these calls.
+ *
+ * Conventions
+ *   - Plain pointers and sizes; no C++ types; no exceptions cross the ABI.
+ *   - Every call returns an int status (BNPP_OK == 0, negative on error);
+ *     bnpp_strerror(status) names it, bnpp_last_error() gives the detail of the
+ *     last failure on the calling thread.
+ *   - Tables are row-major over their scope with the LAST variable fastest
+ *     (domain.cpp:15-26).  Scopes are arrays of variable ids; `cards` is indexed
+ *     by variable id.
+ *   - Device tables passed to the single-op calls are caller-owned device
+ *     buffers (bnpp_malloc, hipMalloc or a torch tensor's data_ptr); the engine
+ *     never frees them.  `stream` is a hipStream_t (NULL: the context stream).
+ *     Single-op calls only enqueue work.
+ *   - No CPU fallback: without a usable MI355X every compute call fails with
+ *     BNPP_ERR_NO_DEVICE.  Model loading, evidence loading, ordering and scope
+ *     rules are host-only and work everywhere.
+ *   - Thread safety: one context per device; calls on distinct contexts or
+ *     distinct streams may run concurrently; model objects are read-only after
+ *     creation.
+ */
+#ifndef BNPP_H
+#define BNPP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BNPP_VERSION 100
+
+enum bnpp_status {
+    BNPP_OK = 0,
+    BNPP_ERR_INVALID = -1,      /* bad shape / argument  (reference: throw const char*, assert) */
+    BNPP_ERR_NO_DEVICE = -2,    /* no usable GPU */
+    BNPP_ERR_OOM = -3,
+    BNPP_ERR_HIP = -4,
+    BNPP_ERR_IO = -5,           /* cannot open / parse a file (io.cpp:124, 150, 177: return -1/-2) */
+    BNPP_ERR_UNSUPPORTED = -6
+};
+
+enum bnpp_dtype { BNPP_F64 = 0, BNPP_F32 = 1 };
+
+/* elimination-order heuristics: bn flags -mf / -wmf / -md (bn.cpp:183-191) */
+enum bnpp_heuristic { BNPP_ORDER_GIVEN = 0, BNPP_MIN_FILL = 1, BNPP_WEIGHTED_MIN_FILL = 2, BNPP_MIN_DEGREE = 3 };
+
+const char *bnpp_strerror(int status);
+const char *bnpp_last_error(void);
+int bnpp_version(void);
+
+/* ------------------------------------------------------------- device */
+typedef struct bnpp_ctx bnpp_ctx;
+
+int bnpp_device_count(int *n);
+int bnpp_ctx_create(int device, bnpp_ctx **out);
+int bnpp_ctx_destroy(bnpp_ctx *ctx);
+int bnpp_ctx_stream(bnpp_ctx *ctx, void **stream);
+int bnpp_malloc(bnpp_ctx *ctx, size_t bytes, void **dptr);
+int bnpp_free(bnpp_ctx *ctx, void *dptr);
+int bnpp_memcpy_h2d(bnpp_ctx *ctx, void *dst, const void *src, size_t bytes);
+int bnpp_memcpy_d2h(bnpp_ctx *ctx, void *dst, const void *src, size_t bytes);
+int bnpp_synchronize(bnpp_ctx *ctx, void *stream);
+
+/* ------------------------------------------------- scope rules (host) */
+/* Output scope of ((Factor(1.0) * in_0) * in_1) ... .sum_out(elim_var):
+ * Domain(d1,d2) union order (domain.cpp:32-52) then Domain(d,v) removal
+ * (domain.cpp:54-72).  elim_var < 0: pure product.  Writes *out_ndims ids. */
+int bnpp_out_scope(int n_in, const int *in_ndims, const int *const *in_vars, int elim_var, int cap,
+                   int *out_ndims, int *out_vars);
+
+/* --------------------------------------------- single ops (device) */
+/* Fused bucket:  out = sum_{elim_var} prod_i in_i   — replaces the bucket body of
+ * BN::variable_elimination (model.cpp:414-418):
+ *     Factor prod(1.0); for (pf : bucket) prod *= *pf; prod.sum_out(var)
+ * i.e. Factor::operator*= (factor.cpp:77-81) + Factor::product (factor.cpp:117-147)
+ * + Factor::sum_out (factor.cpp:182-212) in one pass with no intermediate table.
+ * fp64 results are bit-identical to that chain evaluated in input order.
+ * out_vars must be the layout from bnpp_out_scope (or any permutation of it).
+ * 1 <= n_in <= 8; elim_var < 0 means no summation; elim_var absent from every
+ * input makes it a copy (factor.cpp:185-188). */
+int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, int n_in,
+                          const void *const *in_tables, const int *in_ndims, const int *const *in_vars,
+                          int elim_var, void *out_table, int out_ndims, const int *out_vars);
+
+/* Factor::product (factor.cpp:117-147; factor.hh:35) */
+int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *a, int a_ndims,
+                 const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
+                 const int *out_vars);
+
+/* Factor::sum_out (factor.cpp:182-212; factor.hh:34) */
+int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
+                 const int *vars, int var, void *out, int out_ndims, const int *out_vars);
+
+/* Factor::conditioning (factor.cpp:214-242; factor.hh:38): out scope = vars minus
+ * evidence vars, order preserved (domain.cpp:74-90) */
+int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
+                   const int *vars, int n_ev, const int *ev_vars, const int *ev_vals, void *out);
+
+/* ------------------------------------------------------ models (host) */
+typedef struct bnpp_model bnpp_model;
+
+/* read_uai_model (io.cpp:102-154) without the BAYES/MARKOV split: both kinds load */
+int bnpp_model_load_uai(const char *path, bnpp_model **out);
+/* the same data from arrays: scopes concatenated, values concatenated (row-major) */
+int bnpp_model_from_arrays(int is_bayes, int n_vars, const int *cards, int n_factors, const int *widths,
+                           const int *scopes, const double *values, bnpp_model **out);
+int bnpp_model_free(bnpp_model *m);
+int bnpp_model_info(const bnpp_model *m, int *is_bayes, int *n_vars, int *n_factors);
+int bnpp_model_cards(const bnpp_model *m, int *cards);
+/* read_uai_evidence (io.cpp:157-180): *n pairs (0 unless the first integer is 1) */
+int bnpp_evidence_load(const char *path, int cap, int *n, int *vars, int *vals);
+
+/* Graph::ordering (graph.cpp:41-101) over the graph of the evidence-conditioned
+ * factors, as BN::variable_elimination builds it (model.cpp:360-369).
+ * vars NULL: all non-evidence variables.  *width_out: induced width. */
+int bnpp_ordering(const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals, int n_vars,
+                  const int *vars, int heuristic, int *order_out, int *width_out);
+
+/* ------------------------------------------------ inference (device) */
+/* BN::partition (model.cpp:250-301), VE branch: conditioning + VE.  Messages are
+ * kept resident in HBM and rescaled by exact powers of two, so Z is returned as
+ * log10 (always finite unless Z == 0) and as a double (may overflow to inf, as
+ * the reference's would).  order: explicit order (heuristic BNPP_ORDER_GIVEN),
+ * NULL otherwise.  uptime_ms covers ordering + planning + device run, like the
+ * reference's steady_clock scope (model.cpp:258/296). */
+int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                   int heuristic, const int *order, int n_order, int dtype, double *log10_z, double *z,
+                   double *uptime_ms);
+
+/* BN::marginals (model.cpp:303-346), VE branch: one VE per target with every
+ * other variable eliminated, then Factor::normalize (factor.cpp:244-255).  All
+ * targets run as one batched device schedule.  targets NULL: all variables.
+ * out receives sum(card[t]) values target-major; an evidence variable's marginal
+ * is written one-hot (the UAI MAR format; the reference prints a width-0 factor). */
+int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                   int heuristic, int n_targets, const int *targets, int dtype, double *out, double *uptime_ms);
+
+/* BN::variable_elimination (model.cpp:348-446) over the factors of `m` taken
+ * as given (already conditioned by the caller): eliminates `vars` (heuristic
+ * order, or exactly this order with BNPP_ORDER_GIVEN) and returns the result
+ * factor: *out_ndims scope ids in out_vars (reference chain order), *out_size
+ * values in out_values, scaled: true value = out_values[i] * 2^(*exp2). */
+int bnpp_variable_elimination(bnpp_ctx *ctx, const bnpp_model *m, int n_vars, const int *vars, int heuristic,
+                              int dtype, int cap_vars, int *out_ndims, int *out_vars, int64_t cap_values,
+                              int64_t *out_size, double *out_values, int64_t *exp2);
+
+/* Host-only planning statistics (no device needed): kind 0 partition, 1 marginals
+ * of all variables.  stats as bnpp_job_stats. */
+int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
+                    int dtype, double *stats, int n_stats);
+
+/* ------------------------------------------- prepared jobs (benchmark) */
+/* A planned, device-resident inference that can be launched repeatedly. */
+typedef struct bnpp_job bnpp_job;
+/* kind 0: partition (targets ignored)   kind 1: marginals of `targets` */
+int bnpp_job_create(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars,
+                    const int *ev_vals, int heuristic, const int *order, int n_order, int n_targets,
+                    const int *targets, int dtype, bnpp_job **out);
+/* stats: [0] factor-entries per launch, [1] arena bytes, [2] levels, [3] buckets,
+ *        [4] max induced width, [5] largest message entries, [6] algorithmic bytes */
+int bnpp_job_stats(const bnpp_job *job, double *stats, int n_stats);
+int bnpp_job_launch(bnpp_job *job, void *stream);
+/* waits on stream; partition: out[0] = log10 Z; marginals: sum(card) values */
+int bnpp_job_results(bnpp_job *job, void *stream, double *out);
+int bnpp_job_free(bnpp_job *job);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

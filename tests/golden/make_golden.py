@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Run in the build container (needs /root/reference and `make -C oracle ref`):
+
+    python tests/golden/make_golden.py
+
+It
+  1. copies the reference's own model + fixture files that the tests use into
+     tests/golden/models/ (data: .uai models, .evid evidence, .PR/.MAR outputs),
+  2. writes the synthetic models (bn-pp_amd/python/bnpp/synth.py) next to them,
+  3. runs oracle/_ref/ref_harness (the reference compiled from its sources) for
+     PR / MAR / orderings / single-op known-answer tests, and
+  4. stores inputs and outputs as JSON (values printed with %.17g).
+Nothing here is needed at test time except the JSON and model files it writes.
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.normpath(os.path.join(HERE, "..", ".."))
+REF_MODELS = "/root/reference/models"
+HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+MODELS = os.path.join(HERE, "models")
+sys.path.insert(0, os.path.join(REPO, "bn-pp_amd", "python"))
+from bnpp import synth  # noqa: E402
+
+COPY = {
+    "markovnets": ["grid3x3.uai", "grid3x3-PR.uai.evid", "grid3x3-MAR.uai.evid", "grid3x3.uai.PR", "grid3x3.uai.MAR",
+                   "network.uai", "network.uai.evid", "network.uai.PR", "network.uai.MAR"],
+    "bayesnets": ["asia.uai", "asia.uai.evid", "cancer.uai", "earthquake.uai", "child.uai", "alarm.uai",
+                  "insurance.uai", "win95pts.uai", "hailfinder.uai", "hepar2.uai", "andes.uai", "Water.uai",
+                  "pathfinder.uai"],
+}
+
+
+def run(*args, timeout=900):
+    out = subprocess.run([HARNESS] + [str(a) for a in args], check=True, capture_output=True, text=True,
+                         timeout=timeout)
+    return out.stdout
+
+
+def parse_kv(text):
+    d = {}
+    for line in text.splitlines():
+        parts = line.split()
+        if len(parts) == 2:
+            d[parts[0]] = float(parts[1])
+    return d
+
+
+def parse_factors(text):
+    """lines 'TAG w ids.. | size partition | values..' -> {TAG: {...}}"""
+    res = {}
+    for line in text.splitlines():
+        if "|" not in line:
+            continue
+        head, mid, vals = line.split("|")
+        h = head.split()
+        tag, w = h[0], int(h[1])
+        size, part = mid.split()
+        res[tag] = {"scope": [int(x) for x in h[2:2 + w]], "size": int(size), "partition": float(part),
+                    "values": [float(x) for x in vals.split()]}
+    return res
+
+
+def model_path(name):
+    return os.path.join(MODELS, name)
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        sys.exit("build the reference first: make -C oracle ref")
+    os.makedirs(MODELS, exist_ok=True)
+    for sub, names in COPY.items():
+        for n in names:
+            shutil.copyfile(os.path.join(REF_MODELS, sub, n), model_path(n))
+
+    # synthetic instances (SURVEY.md §8(d) generator)
+    synthetic = {}
+    for n in (4, 5, 6, 8, 10, 12):
+        synthetic["ising%dx%d.uai" % (n, n)] = synth.ising_grid(n, n, seed=0)
+    synthetic["ising12x32.uai"] = synth.ising_grid(12, 32, seed=0)
+    synthetic["potts6x6.uai"] = synth.potts_grid(6, 6, k=4, seed=0)
+    synthetic["potts4x5k3.uai"] = synth.potts_grid(4, 5, k=3, seed=1)
+    synthetic["noisyor_30_40.uai"] = synth.noisy_or_bn(30, 40, 3, seed=0)
+    for name, m in synthetic.items():
+        synth.write_uai(m, model_path(name))
+    # deterministic evidence for the BNs: every 5th variable set to 0 (and 1 for odd ids)
+    rng = random.Random(7)
+    bn_ev = {}
+    for n in ("cancer.uai", "earthquake.uai", "child.uai", "alarm.uai", "insurance.uai", "hailfinder.uai",
+              "noisyor_30_40.uai"):
+        m = synth.read_uai(model_path(n))
+        ev = {}
+        for v in range(len(m["cards"])):
+            if rng.random() < 0.2:
+                ev[v] = rng.randrange(m["cards"][v])
+        name = n + ".evid"
+        synth.write_evidence(ev, model_path(name))
+        bn_ev[n] = name
+    ising_ev = {}
+    for n in (6, 8):
+        ev = {0: 1, n * n // 2: 0, n * n - 1: 1}
+        name = "ising%dx%d.uai.evid" % (n, n)
+        synth.write_evidence(ev, model_path(name))
+        ising_ev["ising%dx%d.uai" % (n, n)] = name
+
+    ve = {"pr": [], "mar": [], "width": []}
+    pr_cases = [("grid3x3.uai", "grid3x3-PR.uai.evid", "mf"), ("grid3x3.uai", "grid3x3-PR.uai.evid", "given"),
+                ("grid3x3.uai", "-", "mf"), ("network.uai", "-", "mf"), ("asia.uai", "asia.uai.evid", "given"),
+                ("asia.uai", "asia.uai.evid", "mf"), ("potts6x6.uai", "-", "mf"), ("potts4x5k3.uai", "-", "wmf"),
+                ("ising12x32.uai", "-", "mf")]
+    for n in (4, 5, 6, 8, 10, 12):
+        pr_cases.append(("ising%dx%d.uai" % (n, n), "-", "mf"))
+    pr_cases += [("ising6x6.uai", "ising6x6.uai.evid", "md"), ("ising8x8.uai", "ising8x8.uai.evid", "wmf")]
+    for n, e in bn_ev.items():
+        pr_cases.append((n, e, "mf"))
+    for n in ("pathfinder.uai", "Water.uai", "hepar2.uai", "win95pts.uai", "andes.uai"):
+        pr_cases.append((n, "-", "mf"))
+    for model, ev, h in pr_cases:
+        r = parse_kv(run("pr", model_path(model), model_path(ev) if ev != "-" else "-", h))
+        ve["pr"].append({"model": model, "evidence": ev, "heuristic": h, "Z": r["Z"], "log10Z": r["log10Z"],
+                         "ref_uptime_ms": r["uptime_ms"]})
+        print("pr", model, ev, h, r["log10Z"])
+
+    mar_cases = [("grid3x3.uai", "grid3x3-MAR.uai.evid", "mf"), ("network.uai", "-", "mf"),
+                 ("asia.uai", "-", "mf"), ("asia.uai", "asia.uai.evid", "given"), ("ising4x4.uai", "-", "mf"),
+                 ("ising6x6.uai", "ising6x6.uai.evid", "mf"), ("ising8x8.uai", "-", "md"),
+                 ("potts4x5k3.uai", "-", "mf"), ("child.uai", bn_ev["child.uai"], "mf"),
+                 ("alarm.uai", bn_ev["alarm.uai"], "wmf"), ("noisyor_30_40.uai", bn_ev["noisyor_30_40.uai"], "mf")]
+    for model, ev, h in mar_cases:
+        txt = run("mar", model_path(model), model_path(ev) if ev != "-" else "-", h)
+        fs = parse_factors(txt)
+        marg = {}
+        for tag, f in fs.items():
+            marg[int(tag[1:])] = {"scope": f["scope"], "values": f["values"]}
+        up = parse_kv(txt).get("uptime_ms")
+        ve["mar"].append({"model": model, "evidence": ev, "heuristic": h, "marginals": marg, "ref_uptime_ms": up})
+        print("mar", model, ev, h, len(marg))
+
+    for model in ("ising8x8.uai", "ising10x10.uai", "ising12x12.uai", "ising12x32.uai", "network.uai", "alarm.uai",
+                  "potts6x6.uai"):
+        for h in ("mf", "wmf", "md"):
+            txt = run("width", model_path(model), h)
+            w = int(txt.split()[1])
+            ve["width"].append({"model": model, "heuristic": h, "width": w})
+    with open(os.path.join(HERE, "ve_golden.json"), "w") as f:
+        json.dump(ve, f, indent=1)
+
+    # ------------------------------------------------- single-op KATs
+    rng = random.Random(12345)
+    lines, cases = [], []
+    cards = {}
+    for v in range(10):
+        cards[v] = rng.randint(2, 5)
+        lines.append("var %d %d" % (v, cards[v]))
+
+    def rand_scope(wmax):
+        w = rng.randint(0, wmax)
+        return rng.sample(range(10), w)
+
+    def size_of(scope):
+        s = 1
+        for v in scope:
+            s *= cards[v]
+        return s
+
+    def rand_values(scope, lo=0.05, hi=3.0):
+        return [rng.uniform(lo, hi) for _ in range(size_of(scope))]
+
+    fid = 0
+
+    def factor(scope, values=None):
+        nonlocal fid
+        name = "F%d" % fid
+        fid += 1
+        vals = values if values is not None else rand_values(scope)
+        lines.append("factor %s %d %s %s" % (name, len(scope), " ".join(map(str, scope)),
+                                            " ".join("%.17g" % x for x in vals)))
+        return name, scope, vals
+
+    for t in range(60):
+        a = factor(rand_scope(4))
+        b = factor(rand_scope(4))
+        out = "P%d" % t
+        lines.append("product %s %s %s" % (out, a[0], b[0]))
+        lines.append("print %s" % out)
+        case = {"op": "product", "a": a[0], "b": b[0], "out": out}
+        # sum out a random variable of the union (or one that is absent)
+        un = a[1] + [v for v in b[1] if v not in a[1]]
+        x = rng.choice(un) if un and rng.random() < 0.85 else rng.randrange(10)
+        so = "S%d" % t
+        lines.append("sum_out %s %s %d" % (so, out, x))
+        lines.append("print %s" % so)
+        cases.append(case)
+        cases.append({"op": "sum_out", "a": out, "var": x, "out": so})
+        # conditioning on up to 2 variables (some outside the scope)
+        ev = {}
+        for v in rng.sample(range(10), rng.randint(0, 3)):
+            ev[v] = rng.randrange(cards[v])
+        co = "C%d" % t
+        lines.append("cond %s %s %d %s" % (co, a[0], len(ev), " ".join("%d %d" % kv for kv in sorted(ev.items()))))
+        lines.append("print %s" % co)
+        cases.append({"op": "cond", "a": a[0], "evidence": {str(k): v for k, v in ev.items()}, "out": co})
+        no = "N%d" % t
+        lines.append("normalize %s %s" % (no, b[0]))
+        lines.append("print %s" % no)
+        cases.append({"op": "normalize", "a": b[0], "out": no})
+        do = "D%d" % t
+        lines.append("divide %s %s %s" % (do, a[0], b[0]))
+        lines.append("print %s" % do)
+        cases.append({"op": "divide", "a": a[0], "b": b[0], "out": do})
+    # buckets: chains of 2..5 factors then sum_out (model.cpp:414-418)
+    for t in range(40):
+        m = rng.randint(2, 5)
+        fs = [factor(rand_scope(3)) for _ in range(m)]
+        un = []
+        for f in fs:
+            un += [v for v in f[1] if v not in un]
+        if not un:
+            continue
+        x = rng.choice(un)
+        cur = fs[0][0]
+        for i, f in enumerate(fs[1:]):
+            nxt = "B%d_%d" % (t, i)
+            lines.append("product %s %s %s" % (nxt, cur, f[0]))
+            cur = nxt
+        out = "M%d" % t
+        lines.append("sum_out %s %s %d" % (out, cur, x))
+        lines.append("print %s" % out)
+        cases.append({"op": "bucket", "inputs": [f[0] for f in fs], "var": x, "out": out})
+    factors = {}
+    for line in lines:
+        p = line.split()
+        if p[0] == "factor":
+            w = int(p[2])
+            factors[p[1]] = {"scope": [int(x) for x in p[3:3 + w]], "values": [float(x) for x in p[3 + w:]]}
+    opfile = os.path.join("/tmp", "bnpp_kat_ops.txt")
+    with open(opfile, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    outs = parse_factors(run("kat", opfile))
+    with open(os.path.join(HERE, "kat_golden.json"), "w") as f:
+        json.dump({"cards": {str(k): v for k, v in cards.items()}, "factors": factors, "cases": cases,
+                   "outputs": outs}, f)
+    print("kat cases", len(cases), "outputs", len(outs))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,319 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference's golden vectors.
+
+Tolerances (north star: index arithmetic bit-exact, PR/MAR within 1e-6 rel):
+  * fp64: bit-exact against the oracle for single ops, buckets and whole VE runs
+    (same elimination order, same chain order, -ffp-contract=off kernels, exact
+    power-of-two rescaling); against the reference's own golden values 1e-12
+    relative on Z (the reference may multiply >=3-factor chains in another order).
+  * fp32: 1e-6 relative on single-op values, 1e-6 relative on log10 Z,
+    1e-5 absolute on marginals.
+"""
+import math
+import random
+
+import pytest
+import torch
+
+import bnpp
+import refcpu
+from conftest import evidence_of, model_path
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+TD = {bnpp.F64: torch.float64, bnpp.F32: torch.float32}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(vals, dtype):
+    return torch.tensor(vals, dtype=TD[dtype], device=DEV)
+
+
+def _cards_list(cards: dict):
+    n = max(cards) + 1
+    return [cards.get(v, 1) for v in range(n)]
+
+
+def run_bucket(ctx, dtype, cards, inputs, elim, out_vars=None):
+    """inputs: [(scope, values)] -> (out_scope, values list)"""
+    scopes = [s for s, _ in inputs]
+    if out_vars is None:
+        out_vars = bnpp.out_scope(scopes, elim)
+    size = 1
+    for v in out_vars:
+        size *= cards[v]
+    tabs = [_dev(vals, dtype) for _, vals in inputs]
+    out = torch.full((size,), float("nan"), dtype=TD[dtype], device=DEV)
+    bnpp.bucket_eliminate(ctx, dtype, _cards_list(cards), [t.data_ptr() for t in tabs], scopes, elim,
+                          out.data_ptr(), out_vars, stream=_stream())
+    torch.cuda.synchronize()
+    return out_vars, out.cpu().tolist()
+
+
+# ------------------------------------------------------------ single ops
+@pytest.mark.parametrize("dtype", [bnpp.F64, bnpp.F32])
+def test_kat_single_ops(ctx, golden_kat, dtype):
+    cards = {int(k): v for k, v in golden_kat["cards"].items()}
+    facs = golden_kat["factors"]
+    outs = golden_kat["outputs"]
+    products = {}
+    checked = 0
+    for case in golden_kat["cases"]:
+        ref = outs[case["out"]]
+        op = case["op"]
+        if op == "product":
+            a, b = facs[case["a"]], facs[case["b"]]
+            scope, vals = run_bucket(ctx, dtype, cards, [(a["scope"], a["values"]), (b["scope"], b["values"])], -1)
+            products[case["out"]] = (scope, ref["values"])     # feed sum_out the reference's exact table
+        elif op == "sum_out":
+            s, v = products[case["a"]]
+            scope, vals = run_bucket(ctx, dtype, cards, [(s, v)], case["var"])
+        elif op == "bucket":
+            ins = [(facs[x]["scope"], facs[x]["values"]) for x in case["inputs"]]
+            scope, vals = run_bucket(ctx, dtype, cards, ins, case["var"])
+        elif op == "cond":
+            a = facs[case["a"]]
+            ev = {int(k): v for k, v in case["evidence"].items()}
+            scope = [v for v in a["scope"] if v not in ev]
+            size = 1
+            for v in scope:
+                size *= cards[v]
+            t = _dev(a["values"], dtype)
+            out = torch.full((size,), float("nan"), dtype=TD[dtype], device=DEV)
+            bnpp.condition(ctx, dtype, _cards_list(cards), t.data_ptr(), a["scope"], ev, out.data_ptr(),
+                           stream=_stream())
+            torch.cuda.synchronize()
+            vals = out.cpu().tolist()
+        else:
+            continue                      # normalize / divide: host bookkeeping, not on the device path
+        assert scope == ref["scope"], case
+        if dtype == bnpp.F64:
+            assert vals == ref["values"], case
+        else:
+            for x, y in zip(vals, ref["values"]):
+                assert abs(x - y) <= 1e-6 * abs(y) + 1e-30, (case, x, y)
+        checked += 1
+    assert checked >= 200
+
+
+def _rand_bucket(rng, n_vars=12):
+    cards = {v: rng.randint(2, 5) for v in range(n_vars)}
+    n_in = rng.randint(1, 8)
+    ins = []
+    for _ in range(n_in):
+        w = rng.randint(0, 4)
+        scope = rng.sample(range(n_vars), w)
+        size = 1
+        for v in scope:
+            size *= cards[v]
+        ins.append((scope, [rng.uniform(0.1, 2.0) for _ in range(size)]))
+    union = []
+    for s, _ in ins:
+        union += [v for v in s if v not in union]
+    elim = rng.choice(union) if union and rng.random() < 0.8 else -1
+    return cards, ins, elim
+
+
+def test_random_buckets_bit_exact_vs_oracle(ctx):
+    rng = random.Random(2024)
+    for it in range(150):
+        cards, ins, elim = _rand_bucket(rng)
+        scope, vals = run_bucket(ctx, bnpp.F64, cards, ins, elim)
+        fs = [refcpu.Factor.new(s, cards, v) for s, v in ins]
+        if elim >= 0:
+            ref = refcpu.bucket(fs, elim, cards[elim])
+        else:
+            ref = fs[0]
+            for f in fs[1:]:
+                ref = ref.product(f)
+        assert scope == ref.scope, it
+        assert vals == ref.values, it
+
+
+def test_permuted_output_layout(ctx):
+    """Any permutation of the output scope is accepted and gives the same table, transposed."""
+    rng = random.Random(5)
+    for it in range(30):
+        cards, ins, elim = _rand_bucket(rng, 8)
+        scope, vals = run_bucket(ctx, bnpp.F64, cards, ins, elim)
+        if len(scope) < 2:
+            continue
+        perm = scope[:]
+        rng.shuffle(perm)
+        pscope, pvals = run_bucket(ctx, bnpp.F64, cards, ins, elim, out_vars=perm)
+        t = torch.tensor(vals, dtype=torch.float64).reshape([cards[v] for v in scope])
+        t = t.permute([scope.index(v) for v in perm]).reshape(-1)
+        assert pvals == t.tolist(), it
+
+
+def test_sum_out_absent_variable_is_copy(ctx):
+    cards = {0: 3, 1: 2, 2: 4}
+    vals = [float(i + 1) for i in range(6)]
+    scope, out = run_bucket(ctx, bnpp.F64, cards, [([0, 1], vals)], 2)
+    assert scope == [0, 1] and out == vals
+
+
+def test_width_zero_and_unit_factors(ctx):
+    cards = {0: 2, 1: 3}
+    scope, out = run_bucket(ctx, bnpp.F64, cards, [([], [2.5]), ([], [4.0])], -1)
+    assert scope == [] and out == [10.0]
+    scope, out = run_bucket(ctx, bnpp.F64, cards, [([], [2.0]), ([0], [1.0, 3.0])], 0)
+    assert scope == [] and out == [8.0]
+
+
+def test_invalid_shapes_rejected(ctx):
+    a = _dev([1.0, 2.0], bnpp.F64)
+    out = _dev([0.0, 0.0], bnpp.F64)
+    with pytest.raises(bnpp.BnppError) as e:       # output scope is not union minus elim
+        bnpp.bucket_eliminate(ctx, bnpp.F64, [2, 2], [a.data_ptr()], [[0]], -1, out.data_ptr(), [1])
+    assert e.value.status == bnpp.ERR_INVALID
+    with pytest.raises(bnpp.BnppError):            # more than 8 inputs
+        bnpp.bucket_eliminate(ctx, bnpp.F64, [2], [a.data_ptr()] * 9, [[0]] * 9, -1, out.data_ptr(), [0])
+
+
+# ----------------------------------------------------------- whole VE runs
+FAST_PR = [c for c in ["grid3x3.uai", "network.uai", "asia.uai", "potts6x6.uai", "potts4x5k3.uai", "ising4x4.uai",
+                       "ising5x5.uai", "ising6x6.uai", "ising8x8.uai", "ising10x10.uai", "ising12x12.uai",
+                       "cancer.uai", "earthquake.uai", "child.uai", "alarm.uai", "insurance.uai", "hailfinder.uai",
+                       "noisyor_30_40.uai", "pathfinder.uai", "Water.uai", "hepar2.uai", "win95pts.uai",
+                       "andes.uai"]]
+
+
+def _pr_cases(golden_ve, models=None):
+    return [c for c in golden_ve["pr"] if models is None or c["model"] in models]
+
+
+def test_partition_fp64_bit_exact(ctx, golden_ve):
+    n = 0
+    for case in _pr_cases(golden_ve, FAST_PR):
+        m = bnpp.Model.load(model_path(case["model"]))
+        ev = evidence_of(case["evidence"])
+        lz, z, _ = bnpp.partition(ctx, m, ev, case["heuristic"], bnpp.F64)
+        rz, _ = refcpu.Model.load(model_path(case["model"])).partition(ev, case["heuristic"])
+        assert z == rz, (case, z, rz)                                     # oracle: bit-exact
+        assert abs(z - case["Z"]) <= 1e-12 * abs(case["Z"]), (case, z)     # reference: chain-order rounding
+        assert abs(lz - math.log10(rz)) <= 1e-12 * max(1.0, abs(lz))
+        n += 1
+    assert n >= 20
+
+
+def test_partition_strip_12x32(ctx, golden_ve):
+    """BASELINE config 3 restated: the reference-runnable 32x12 strip."""
+    case = _pr_cases(golden_ve, {"ising12x32.uai"})[0]
+    m = bnpp.Model.load(model_path(case["model"]))
+    lz, z, _ = bnpp.partition(ctx, m, {}, "mf", bnpp.F64)
+    assert abs(z - case["Z"]) <= 1e-12 * abs(case["Z"])
+    lz32, _, _ = bnpp.partition(ctx, m, {}, "mf", bnpp.F32)
+    assert abs(lz32 - case["log10Z"]) <= 1e-6 * abs(case["log10Z"])
+
+
+def test_partition_fp32_within_tolerance(ctx, golden_ve):
+    for case in _pr_cases(golden_ve, FAST_PR):
+        m = bnpp.Model.load(model_path(case["model"]))
+        lz, _, _ = bnpp.partition(ctx, m, evidence_of(case["evidence"]), case["heuristic"], bnpp.F32)
+        assert abs(lz - case["log10Z"]) <= 1e-6 * max(1.0, abs(case["log10Z"])), (case, lz)
+
+
+@pytest.mark.parametrize("dtype", [bnpp.F64, bnpp.F32])
+def test_marginals_vs_golden(ctx, golden_ve, dtype):
+    for case in golden_ve["mar"]:
+        m = bnpp.Model.load(model_path(case["model"]))
+        ev = evidence_of(case["evidence"])
+        marg, _ = bnpp.marginals(ctx, m, ev, case["heuristic"], dtype)
+        if dtype == bnpp.F64:
+            rm, _ = refcpu.Model.load(model_path(case["model"])).marginals(ev, case["heuristic"])
+        for t, ref in case["marginals"].items():
+            t = int(t)
+            if not ref["scope"]:
+                assert marg[t][ev[t]] == 1.0 and sum(marg[t]) == 1.0
+                continue
+            if dtype == bnpp.F64:
+                assert marg[t] == rm[t], (case["model"], t)                # oracle: bit-exact
+                tol = 1e-13
+            else:
+                tol = 1e-5
+            for a, b in zip(marg[t], ref["values"]):
+                assert abs(a - b) <= tol, (case["model"], t, marg[t], ref["values"])
+
+
+def test_reference_fixture_files(ctx):
+    """models/markovnets/grid3x3.uai.PR = 14.8899, network.uai.PR = 163.204 (log10 Z)."""
+    for name, ev in (("grid3x3.uai", "grid3x3-PR.uai.evid"), ("network.uai", "network.uai.evid")):
+        m = bnpp.Model.load(model_path(name))
+        lz, _, _ = bnpp.partition(ctx, m, bnpp.load_evidence(model_path(ev)), "mf", bnpp.F64)
+        want = float(open(model_path(name + ".PR")).read().split()[-1])
+        assert round(lz, 4 if abs(want) < 100 else 3) == want
+
+
+def test_job_relaunch_is_idempotent(ctx):
+    m = bnpp.Model.load(model_path("ising10x10.uai"))
+    job = bnpp.Job(ctx, m, "pr", heuristic="mf", dtype=bnpp.F64)
+    job.launch()
+    a = job.results()
+    for _ in range(3):
+        job.launch()
+    b = job.results()
+    assert a == b
+    job.close()
+
+
+# ------------------------------------------------ size-independent properties
+def test_order_independence_20x20(ctx):
+    """log10 Z of a 20x20 grid (beyond the oracle's reach) agrees across
+    elimination orders (different buckets, layouts and message shapes)."""
+    from bnpp import synth
+    m = bnpp.Model.from_dict(synth.ising_grid(20, 20, seed=3))
+    vals = [bnpp.partition(ctx, m, {}, h, bnpp.F64)[0] for h in ("mf", "wmf", "md")]
+    col = [c * 20 + r for c in range(20) for r in range(20)]                 # column sweep, width 20
+    vals.append(bnpp.partition(ctx, m, {}, "mf", bnpp.F64, order=col)[0])
+    for v in vals[1:]:
+        assert abs(v - vals[0]) <= 1e-10 * abs(vals[0]), vals
+    v32 = bnpp.partition(ctx, m, {}, "mf", bnpp.F32)[0]
+    assert abs(v32 - vals[0]) <= 1e-6 * abs(vals[0])
+
+
+def test_marginals_normalised_and_consistent_14x14(ctx):
+    """MAR on a 14x14 grid: every marginal sums to 1, and the marginal of the
+    last variable matches Z(x=k)/Z computed by conditioned partitions."""
+    from bnpp import synth
+    m = bnpp.Model.from_dict(synth.ising_grid(14, 14, seed=4))
+    marg, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    for t, p in marg.items():
+        assert abs(sum(p) - 1.0) < 1e-12
+    lz = bnpp.partition(ctx, m, {}, "mf", bnpp.F64)[0]
+    t = 195
+    for k in range(2):
+        lzk = bnpp.partition(ctx, m, {t: k}, "mf", bnpp.F64)[0]
+        assert abs(10 ** (lzk - lz) - marg[t][k]) < 1e-12
+
+
+@pytest.mark.parametrize("k,w", [(2, 22), (4, 11)])
+def test_micro_bucket_checksum(ctx, k, w):
+    """Fused m(x,S)*f(x,y) -> sum_x at large size: checksum of checksums
+    sum_out = sum_x (sum_S m[x,S]) * (sum_y f[x,y]), plus sampled entries."""
+    g = torch.Generator(device=DEV).manual_seed(0)
+    S = k ** w
+    for dtype in (bnpp.F64, bnpp.F32):
+        m_t = torch.rand(k * S, generator=g, device=DEV, dtype=TD[dtype]) * 1.5 + 0.5
+        f_t = torch.rand(k * k, generator=g, device=DEV, dtype=TD[dtype]) * 1.5 + 0.5
+        out = torch.empty(S * k, device=DEV, dtype=TD[dtype])
+        cards = [k] * (w + 2)
+        sm = list(range(w + 1))
+        sf = [0, w + 1]
+        bnpp.bucket_eliminate(ctx, dtype, cards, [m_t.data_ptr(), f_t.data_ptr()], [sm, sf], 0, out.data_ptr(),
+                              list(range(1, w + 2)), stream=_stream())
+        torch.cuda.synchronize()
+        M = m_t.double().reshape(k, S)
+        F = f_t.double().reshape(k, k)
+        want = (M.sum(1) * F.sum(1)).sum().item()
+        got = out.double().sum().item()
+        assert abs(got - want) <= (1e-9 if dtype == bnpp.F64 else 1e-4) * want
+        idx = torch.randint(0, S * k, (4096,), generator=g, device=DEV)
+        s_i, y_i = idx // k, idx % k
+        ref = (M[:, s_i] * F[:, y_i]).sum(0)
+        assert torch.allclose(out[idx].double(), ref, rtol=1e-12 if dtype == bnpp.F64 else 1e-6)
+        del m_t, out

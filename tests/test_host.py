@@ -1,0 +1,125 @@
+"""CPU tests of the product library's host side: the C ABI exports, loud
+failure without a GPU, scope rules, UAI/evidence loading, ordering, planning."""
+import os
+import re
+
+import pytest
+
+import bnpp
+import refcpu
+from bnpp import synth
+from conftest import REPO, evidence_of, model_path
+
+
+def _header_functions():
+    txt = open(os.path.join(REPO, "include", "bnpp.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char \*|const char\*)\s*(bnpp_\w+)\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    names = _header_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(bnpp._lib, n), n
+    # and the Python binding declares them all
+    assert set(names) <= set(bnpp.EXPORTED)
+
+
+def test_no_cpu_fallback_without_gpu():
+    if bnpp.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(bnpp.BnppError) as e:
+        bnpp.Context(0)
+    assert e.value.status == bnpp.ERR_NO_DEVICE
+
+
+def test_out_scope_matches_reference_rules(golden_kat):
+    facs = golden_kat["factors"]
+    outs = golden_kat["outputs"]
+    scopes = {}
+    for case in golden_kat["cases"]:
+        ref = outs[case["out"]]["scope"]
+        if case["op"] == "product":
+            s = bnpp.out_scope([facs[case["a"]]["scope"], facs[case["b"]]["scope"]])
+            scopes[case["out"]] = s
+            assert s == ref
+        elif case["op"] == "sum_out":
+            assert bnpp.out_scope([scopes[case["a"]]], case["var"]) == ref
+        elif case["op"] == "bucket":
+            assert bnpp.out_scope([facs[x]["scope"] for x in case["inputs"]], case["var"]) == ref
+
+
+@pytest.mark.parametrize("name", ["grid3x3.uai", "network.uai", "asia.uai", "alarm.uai", "pathfinder.uai",
+                                  "ising12x32.uai", "potts6x6.uai", "noisyor_30_40.uai"])
+def test_uai_loader(name):
+    m = bnpp.Model.load(model_path(name))
+    py = synth.read_uai(model_path(name))
+    assert m.n_vars == len(py["cards"])
+    assert m.n_factors == len(py["scopes"])
+    assert m.cards == py["cards"]
+    assert m.is_bayes == (py["type"] == "BAYES")
+
+
+def test_uai_loader_errors(tmp_path):
+    with pytest.raises(bnpp.BnppError) as e:
+        bnpp.Model.load(str(tmp_path / "missing.uai"))
+    assert e.value.status == bnpp.ERR_IO
+    bad = tmp_path / "bad.uai"
+    bad.write_text("MARKOV\n2\n2 2\n1\n2 0 1\n3\n1 2 3\n")      # 3 values for a 4-entry table
+    with pytest.raises(bnpp.BnppError):
+        bnpp.Model.load(str(bad))
+    hdr = tmp_path / "hdr.uai"
+    hdr.write_text("# comment line\nMARKOV # trailing\n1\n2\n1\n1 0\n2\n0.5 # c\n 1.5\n")
+    m = bnpp.Model.load(str(hdr))
+    assert m.n_vars == 1 and m.cards == [2]
+
+
+def test_evidence_loader(tmp_path):
+    for name in ("grid3x3-PR.uai.evid", "grid3x3-MAR.uai.evid", "asia.uai.evid", "network.uai.evid"):
+        assert bnpp.load_evidence(model_path(name)) == synth.read_evidence(model_path(name))
+    p = tmp_path / "two.evid"
+    p.write_text("2\n1 0 1\n")          # sample count != 1: nothing is read (io.cpp:164)
+    assert bnpp.load_evidence(str(p)) == {}
+
+
+@pytest.mark.parametrize("name", ["ising8x8.uai", "ising10x10.uai", "ising12x32.uai", "network.uai", "alarm.uai",
+                                  "potts6x6.uai", "hailfinder.uai", "noisyor_30_40.uai"])
+@pytest.mark.parametrize("h", ["mf", "wmf", "md"])
+def test_ordering_identical_to_oracle(name, h):
+    """Same selection rules and tie breaks as the oracle's restatement of
+    graph.cpp:41-195, so the orders are identical, not just equally wide."""
+    m = bnpp.Model.load(model_path(name))
+    rm = refcpu.Model.load(model_path(name))
+    order, width = bnpp.ordering(m, {}, h)
+    ro, rw = rm.ordering(list(range(rm.n_vars)), h)
+    assert order == ro
+    assert width == rw
+
+
+def test_ordering_with_evidence_skips_evidence_vars():
+    m = bnpp.Model.load(model_path("grid3x3.uai"))
+    ev = evidence_of("grid3x3-PR.uai.evid")
+    order, width = bnpp.ordering(m, ev, "mf")
+    assert sorted(order) == sorted(v for v in range(9) if v not in ev)
+    assert width >= 1
+
+
+def test_plan_stats():
+    m = bnpp.Model.load(model_path("ising10x10.uai"))
+    st = bnpp.plan_stats(m, 0, {}, "mf")
+    entries, arena, levels, buckets, width = st[:5]
+    _, w = bnpp.ordering(m, {}, "mf")
+    assert width == w == 13
+    assert buckets >= 99 and levels >= 1 and entries > 0 and arena > 0
+    st_mar = bnpp.plan_stats(m, 1, {}, "mf")
+    assert st_mar[3] > 50 * buckets          # one VE per target, batched
+
+
+def test_bad_arguments_are_rejected():
+    m = bnpp.Model.load(model_path("grid3x3.uai"))
+    with pytest.raises(bnpp.BnppError) as e:
+        bnpp.ordering(m, {0: 5}, "mf")      # value out of range
+    assert e.value.status == bnpp.ERR_INVALID
+    with pytest.raises(bnpp.BnppError) as e:
+        bnpp.plan_stats(m, 7)                # unknown job kind
+    assert e.value.status == bnpp.ERR_INVALID
