@@ -88,7 +88,8 @@ def main():
     cards = [k] * (w + 2)
     scope_m, scope_f = list(range(w + 1)), [0, w + 1]
     out_vars = list(range(1, w + 2))
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)              # a real (non-null) stream: kernels and events share it
+    torch.cuda.synchronize(dev)
 
     def step():
         bnpp.bucket_eliminate(ctx, dt, cards, [m_t.data_ptr(), f_t.data_ptr()], [scope_m, scope_f], 0,

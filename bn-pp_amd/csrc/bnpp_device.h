@@ -12,6 +12,11 @@
 #pragma once
 #include <stdint.h>
 
+#if !defined(__HIPCC__) && !defined(__host__)
+#define __host__
+#define __device__
+#endif
+
 namespace bnpp {
 
 constexpr int kMaxIn = 8;          // inputs per fused launch; longer chains are split
@@ -33,17 +38,39 @@ enum BucketFlags : int32_t {
     kTrackMax = 2,     // raise meta[out].maxbits
 };
 
+// Each thread evaluates a V1 x V2 register tile of the output: V1 entries of
+// the fastest output dim times V2 entries of the next one (V2 > 1 only when
+// V1 covers the whole fastest dim, so a tile is V1*V2 contiguous entries).
 struct BucketDesc {
     int64_t out_size;               // entries of the output table
-    int64_t n_vec;                  // out_size / vec
+    int64_t n_tiles;                // out_size / (v1 * v2)
     int64_t vblk_begin;             // first virtual block of this bucket within its launch
-    int32_t n_in, n_dims, k, vec;   // k = card of the summed variable (1: pure product)
+    int64_t tdiv0[2], tdiv1[2];     // divisors card0/v1 and card1/v2 (dim header, magic)
+    int32_t n_in, n_dims, k, v1, v2;// k = card of the summed variable (1: pure product)
     int32_t out_table, flags;
     int32_t in_table[kMaxIn];
     int64_t in_base[kMaxIn];        // evidence offset of each view
     int64_t elim_stride[kMaxIn];    // stride of the summed variable in each view (0: absent)
     int64_t dim_off;                // offset into the dims pool
+    // stream form (big >= 0): input `big` is read from HBM with loads of class
+    // bcls; every other input is copied whole into LDS once per workgroup
+    int32_t big, bcls;
+    int32_t small_elems;            // LDS elements for the small inputs
+    int32_t in_lds_off[kMaxIn];     // element offset of each small input in LDS
+    int32_t in_span[kMaxIn];        // elements of each small input's reachable range
 };
+
+// loads of the big input of a stream bucket, relative to one thread's tile
+enum BigClass : int32_t { kBigRow = 1, kBigCol = 2, kBigFull = 3, kBigDirect = 4 };
+constexpr int kStreamSmallMax = 4096;      // entries: inputs at most this big go to LDS
+constexpr int kStreamLdsBudget = 32768;    // bytes of LDS for the small inputs
+
+// Kernel variant: one instantiation per (input-count class, v1, v2) so every
+// launch gets the register allocation of its own shape.
+__host__ __device__ inline int nin_class(int n_in) { return n_in <= 1 ? 1 : n_in <= 2 ? 2 : n_in <= 4 ? 4 : 8; }
+__host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return nin_class(n_in) * 64 + v1 * 8 + v2; }
+// stream kernels: 4096 + big-class * 64 + v1 * 8 + v2
+__host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 64 + v1 * 8 + v2; }
 
 // dims pool, per output dim (fastest first): 2 + n_in int64 words
 //   w0 = card | (shift << 32) | (pow2 << 40)    w1 = magic    w2.. = stride per input

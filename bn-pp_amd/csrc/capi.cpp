@@ -198,7 +198,7 @@ int plan_schedule(const ModelData &d, const std::vector<int> &ev, int kind, int 
     if (!build_schedule(pp, d.cards, src_sizes, eb, max_vec_for(dtype), s, &msg)) return set_err(BNPP_ERR_INVALID, msg);
     stats[0] = s.entries;
     stats[1] = (double)s.arena_bytes;
-    stats[2] = (double)s.level_vblocks.size();
+    stats[2] = (double)s.n_levels;
     stats[3] = (double)s.descs.size();
     stats[4] = width;
     int64_t mx = 0;

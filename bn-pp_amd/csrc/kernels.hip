@@ -21,6 +21,8 @@
 // loads, stride-0 inputs are broadcast, anything else is gathered.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "bnpp_device.h"
 #include "runtime.hpp"
 
@@ -44,34 +46,44 @@ template <> struct FBits<double> {
     }
 };
 
-template <typename T, int N> struct VecT;
-template <> struct VecT<float, 1> { using type = float; };
-template <> struct VecT<float, 2> { using type = float2; };
-template <> struct VecT<float, 4> { using type = float4; };
-template <> struct VecT<double, 1> { using type = double; };
-template <> struct VecT<double, 2> { using type = double2; };
-
-template <typename T, int VEC>
-__device__ __forceinline__ void load_vec(const T *p, T (&x)[VEC]) {
-    if constexpr (VEC == 1) {
-        x[0] = p[0];
+// N contiguous elements through 16-byte (or narrower) vector accesses.
+template <typename T, int N>
+__device__ __forceinline__ void load_n(const T *p, T *x) {
+    if constexpr (sizeof(T) == 4 && N % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < N / 4; ++c) {
+            float4 v = reinterpret_cast<const float4 *>(p)[c];
+            x[4 * c] = v.x; x[4 * c + 1] = v.y; x[4 * c + 2] = v.z; x[4 * c + 3] = v.w;
+        }
+    } else if constexpr (N % 2 == 0) {
+        using V2 = typename std::conditional<sizeof(T) == 4, float2, double2>::type;
+#pragma unroll
+        for (int c = 0; c < N / 2; ++c) {
+            V2 v = reinterpret_cast<const V2 *>(p)[c];
+            x[2 * c] = v.x; x[2 * c + 1] = v.y;
+        }
     } else {
-        using V = typename VecT<T, VEC>::type;
-        V v = *reinterpret_cast<const V *>(p);
-        if constexpr (VEC == 2) { x[0] = v.x; x[1] = v.y; }
-        if constexpr (VEC == 4) { x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w; }
+#pragma unroll
+        for (int c = 0; c < N; ++c) x[c] = p[c];
     }
 }
-template <typename T, int VEC>
-__device__ __forceinline__ void store_vec(T *p, const T (&x)[VEC]) {
-    if constexpr (VEC == 1) {
-        p[0] = x[0];
+template <typename T, int N>
+__device__ __forceinline__ void store_n(T *p, const T *x) {
+    if constexpr (sizeof(T) == 4 && N % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < N / 4; ++c)
+            reinterpret_cast<float4 *>(p)[c] = make_float4(x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]);
+    } else if constexpr (N % 2 == 0) {
+        using V2 = typename std::conditional<sizeof(T) == 4, float2, double2>::type;
+#pragma unroll
+        for (int c = 0; c < N / 2; ++c) {
+            V2 v;
+            v.x = x[2 * c]; v.y = x[2 * c + 1];
+            reinterpret_cast<V2 *>(p)[c] = v;
+        }
     } else {
-        using V = typename VecT<T, VEC>::type;
-        V v;
-        if constexpr (VEC == 2) { v.x = x[0]; v.y = x[1]; }
-        if constexpr (VEC == 4) { v.x = x[0]; v.y = x[1]; v.z = x[2]; v.w = x[3]; }
-        *reinterpret_cast<V *>(p) = v;
+#pragma unroll
+        for (int c = 0; c < N; ++c) p[c] = x[c];
     }
 }
 
@@ -101,88 +113,175 @@ __device__ __forceinline__ void divmod_dim(uint64_t n, int64_t w0, int64_t w1, u
 struct LoadedBucket {
     int64_t base[kMaxIn];
     int64_t es[kMaxIn];
-    int64_t sf[kMaxIn];      // stride on the fastest output dim
+    int64_t s0[kMaxIn];      // stride on the fastest output dim
+    int64_t s1[kMaxIn];      // stride on the second output dim
     const void *ptr[kMaxIn];
     void *out;
-    const int64_t *dims;
-    int64_t n_vec;
-    int n_in, n_dims, k, vec, flags, neg_e;
+    const int64_t *dims;     // dims pool rows, fastest first
+    int64_t n_tiles;
+    int64_t card0, card1;
+    int64_t t0h, t0m, t1h, t1m;
+    int n_in, n_dims, k, v1, v2, flags, neg_e;
 };
 
-template <typename T, int NIN, int VEC>
-__device__ __forceinline__ T eval_vec(const LoadedBucket &b, int64_t vid) {
+// One input's V1 x V2 tile (strides s0 / s1 along output dims 0 / 1), expanded.
+template <typename T, int V1, int V2>
+__device__ __forceinline__ void load_tile(const T *src, int64_t s0, int64_t s1, T (&x)[V1 * V2]) {
+    constexpr int TS = V1 * V2;
+    if (s0 == 0) {
+        if (V2 == 1 || s1 == 0) {                         // broadcast over the tile
+            T y = src[0];
+#pragma unroll
+            for (int j = 0; j < TS; ++j) x[j] = y;
+        } else {
+            T y[V2];
+            if (s1 == 1) load_n<T, V2>(src, y);
+            else {
+#pragma unroll
+                for (int j2 = 0; j2 < V2; ++j2) y[j2] = src[(int64_t)j2 * s1];
+            }
+#pragma unroll
+            for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+                for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = y[j2];
+        }
+    } else if (V1 > 1 && s0 == 1) {                       // contiguous along the fastest dim
+        if (V2 == 1 || s1 == 0) {
+            T y[V1];
+            load_n<T, V1>(src, y);
+#pragma unroll
+            for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+                for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = y[j1];
+        } else {
+#pragma unroll
+            for (int j2 = 0; j2 < V2; ++j2) load_n<T, V1>(src + (int64_t)j2 * s1, x + j2 * V1);
+        }
+    } else {                                              // general gather
+#pragma unroll
+        for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+            for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = src[(int64_t)j1 * s0 + (int64_t)j2 * s1];
+    }
+}
+
+// Evaluate one V1 x V2 output tile: decode its mixed-radix position once, then
+// run the reference's product chain and sum in the reference's order.
+template <typename T, int NIN, int V1, int V2>
+__device__ __forceinline__ T compute_tile(const LoadedBucket &b, int64_t tid, T (&acc)[V1 * V2]) {
+    constexpr int TS = V1 * V2;
     int64_t pos[NIN];
 #pragma unroll
     for (int i = 0; i < NIN; ++i) pos[i] = b.base[i];
-    uint64_t rem = (uint64_t)vid * VEC;
-    const int64_t *dp = b.dims;
-    for (int j = 0; j < b.n_dims; ++j) {
+    int64_t obase = 0;
+    if (b.n_dims > 0) {
         uint64_t q, r;
-        divmod_dim(rem, dp[0], dp[1], q, r);
+        divmod_dim((uint64_t)tid, b.t0h, b.t0m, q, r);
+        int64_t i0 = (int64_t)r * V1;
 #pragma unroll
-        for (int i = 0; i < NIN; ++i) pos[i] += (int64_t)r * dp[2 + i];
-        rem = q;
-        dp += 2 + NIN;
-    }
-
-    T acc[VEC];
+        for (int i = 0; i < NIN; ++i) pos[i] += i0 * b.s0[i];
+        obase = i0;
+        if (b.n_dims > 1) {
+            uint64_t q1, r1;
+            divmod_dim(q, b.t1h, b.t1m, q1, r1);
+            int64_t i1 = (int64_t)r1 * V2;
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] = T(0);
-    for (int v = 0; v < b.k; ++v) {
-        T p[VEC];
+            for (int i = 0; i < NIN; ++i) pos[i] += i1 * b.s1[i];
+            obase = ((int64_t)q1 * b.card1 + i1) * b.card0 + i0;
+            uint64_t rem = q1;
+            const int row = 2 + b.n_in;                  // dims-pool row length
+            const int64_t *dp = b.dims + 2 * row;
+            for (int j = 2; j < b.n_dims; ++j) {
+                uint64_t qq, rr;
+                divmod_dim(rem, dp[0], dp[1], qq, rr);
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) p[j] = T(1);
-#pragma unroll
-        for (int i = 0; i < NIN; ++i) {
-            const T *src = static_cast<const T *>(b.ptr[i]) + pos[i] + (int64_t)v * b.es[i];
-            if (b.sf[i] == 0) {
-                T x = src[0];
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) p[j] = p[j] * x;
-            } else if (VEC > 1 && b.sf[i] == 1) {
-                T x[VEC];
-                load_vec<T, VEC>(src, x);
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) p[j] = p[j] * x[j];
-            } else {
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) p[j] = p[j] * src[(int64_t)j * b.sf[i]];
+                for (int i = 0; i < NIN; ++i)
+                    if (i < b.n_in) pos[i] += (int64_t)rr * dp[2 + i];
+                rem = qq;
+                dp += row;
             }
         }
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] = acc[j] + p[j];
     }
-    T m = T(0);
+
+#pragma unroll
+    for (int j = 0; j < TS; ++j) acc[j] = T(0);
+    for (int v = 0; v < b.k; ++v) {
+        T p[TS];
+#pragma unroll
+        for (int j = 0; j < TS; ++j) p[j] = T(1);
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) {
+            if (i >= b.n_in) continue;                     // uniform
+            T x[TS];
+            load_tile<T, V1, V2>(static_cast<const T *>(b.ptr[i]) + pos[i] + (int64_t)v * b.es[i], b.s0[i], b.s1[i], x);
+#pragma unroll
+            for (int j = 0; j < TS; ++j) p[j] = p[j] * x[j];
+        }
+#pragma unroll
+        for (int j = 0; j < TS; ++j) acc[j] = acc[j] + p[j];
+    }
     if (b.flags & kScale) {
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] = ldexp_t(acc[j], b.neg_e);
+        for (int j = 0; j < TS; ++j) acc[j] = ldexp_t(acc[j], b.neg_e);
     }
+    (void)obase;                                          // == tid * TS (tiles are enumerated in output order)
+    T m = T(0);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) m = acc[j] > m ? acc[j] : m;
-    store_vec<T, VEC>(static_cast<T *>(b.out) + vid * VEC, acc);
+    for (int j = 0; j < TS; ++j) m = acc[j] > m ? acc[j] : m;
     return m;
 }
 
-template <typename T, int NIN>
-__device__ __forceinline__ T eval_nin(const LoadedBucket &b, int64_t vid) {
-    if (b.vec == 1) return eval_vec<T, NIN, 1>(b, vid);
-    if constexpr (sizeof(T) == 4) {
-        if (b.vec == 4) return eval_vec<T, NIN, 4>(b, vid);
+// LDS image of one wave's output tiles: 64 rows of TS entries, padded by 16 B
+constexpr int kLdsRowPad = 16;
+constexpr int kLdsWaveBytes = 64 * (64 + kLdsRowPad);      // largest tile: 64 B per lane
+
+// Store the wave's tiles (lane l holds tile `wave_tid0 + l`, which covers
+// output entries [tid*TS, tid*TS + TS)).  Tiles of one 16-B access are stored
+// directly (already coalesced); wider tiles go through the wave's LDS image so
+// every global store instruction writes 64 consecutive 16-B chunks.
+template <typename T, int TS>
+__device__ __forceinline__ void store_tiles(T *out, int64_t wave_tid0, int64_t n_tiles, const T (&acc)[TS],
+                                            unsigned char *lds) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tid = wave_tid0 + lane;
+    constexpr int row_bytes = TS * (int)sizeof(T);
+    if constexpr (row_bytes <= 16) {
+        if (tid < n_tiles) store_n<T, TS>(out + tid * TS, acc);
+    } else {
+        constexpr int rowp = row_bytes + kLdsRowPad;
+        constexpr int cpr = row_bytes / 16;                   // 16-B chunks per row
+        constexpr int EPC = 16 / (int)sizeof(T);              // entries per chunk
+        __syncthreads();                                      // previous reads of this image are done
+        store_n<T, TS>(reinterpret_cast<T *>(lds + lane * rowp), acc);
+        __syncthreads();
+        const int64_t valid = n_tiles - wave_tid0;            // tiles of this wave that exist
+#pragma unroll
+        for (int it = 0; it < cpr; ++it) {
+            const int q = it * 64 + lane;                     // chunk index within the wave's region
+            const int src_lane = q / cpr, within = q % cpr;
+            if (src_lane < valid) {
+                T x[EPC];
+                load_n<T, EPC>(reinterpret_cast<const T *>(lds + src_lane * rowp + within * 16), x);
+                store_n<T, EPC>(out + wave_tid0 * TS + (int64_t)q * EPC, x);
+            }
+        }
     }
-    return eval_vec<T, NIN, 2>(b, vid);
 }
 
-template <typename T>
-__device__ __forceinline__ T eval_any(const LoadedBucket &b, int64_t vid) {
-    switch (b.n_in) {
-        case 1: return eval_nin<T, 1>(b, vid);
-        case 2: return eval_nin<T, 2>(b, vid);
-        case 3: return eval_nin<T, 3>(b, vid);
-        case 4: return eval_nin<T, 4>(b, vid);
-        case 5: return eval_nin<T, 5>(b, vid);
-        case 6: return eval_nin<T, 6>(b, vid);
-        case 7: return eval_nin<T, 7>(b, vid);
-        default: return eval_nin<T, 8>(b, vid);
+// fill the per-bucket register state from a descriptor + table pointers
+__device__ __forceinline__ void load_common(LoadedBucket &b, const BucketDesc &d, const int64_t *dims) {
+    b.n_in = d.n_in; b.n_dims = d.n_dims; b.k = d.k; b.v1 = d.v1; b.v2 = d.v2;
+    b.n_tiles = d.n_tiles;
+    b.dims = dims;
+    b.t0h = d.tdiv0[0]; b.t0m = d.tdiv0[1]; b.t1h = d.tdiv1[0]; b.t1m = d.tdiv1[1];
+    b.card0 = d.n_dims > 0 ? (int64_t)((uint64_t)dims[0] & 0xffffffffu) : 1;
+    b.card1 = d.n_dims > 1 ? (int64_t)((uint64_t)dims[2 + d.n_in] & 0xffffffffu) : 1;
+    for (int i = 0; i < kMaxIn; ++i) {
+        bool on = i < d.n_in;
+        b.base[i] = on ? d.in_base[i] : 0;
+        b.es[i] = on ? d.elim_stride[i] : 0;
+        b.s0[i] = on && d.n_dims > 0 ? dims[2 + i] : 0;
+        b.s1[i] = on && d.n_dims > 1 ? dims[2 + d.n_in + 2 + i] : 0;
     }
 }
 
@@ -220,11 +319,12 @@ __device__ __forceinline__ int find_bucket(const BucketDesc *descs, int n_desc, 
     return lo;
 }
 
-template <typename T>
+template <typename T, int NIN, int V1, int V2>
 __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                               const int64_t *__restrict__ pool,
                                                               TableMeta *__restrict__ meta, int64_t total_vblocks) {
     __shared__ T red[kBlock / 64];
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * kLdsWaveBytes];
     LoadedBucket b;
     int cur = -1;
     int64_t cur_begin = 0;
@@ -237,42 +337,45 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
             lmax = T(0);
             const BucketDesc &d = descs[bi];
             cur_begin = d.vblk_begin;
-            b.n_in = d.n_in; b.n_dims = d.n_dims; b.k = d.k; b.vec = d.vec; b.flags = d.flags;
-            b.n_vec = d.n_vec;
-            b.dims = pool + d.dim_off;
+            load_common(b, d, pool + d.dim_off);
+            b.flags = d.flags;
             b.out = meta[d.out_table].ptr;
             int64_t e_sum = 0, x_sum = 0;
             for (int i = 0; i < kMaxIn; ++i) {
                 if (i < d.n_in) {
                     const TableMeta &mi = meta[d.in_table[i]];
                     b.ptr[i] = mi.ptr;
-                    b.base[i] = d.in_base[i];
-                    b.es[i] = d.elim_stride[i];
-                    b.sf[i] = d.n_dims > 0 ? b.dims[2 + i] : 0;
                     int e = FBits<T>::exponent(mi.maxbits);
-                    e_sum += e;
-                    x_sum += mi.exp2 + e;
+                    if (d.flags & kScale) {
+                        e_sum += e;
+                        x_sum += mi.exp2 + e;
+                    } else {
+                        x_sum += mi.exp2;
+                    }
                 } else {
-                    b.ptr[i] = nullptr; b.base[i] = 0; b.es[i] = 0; b.sf[i] = 0;
+                    b.ptr[i] = nullptr;
                 }
             }
-            if (!(d.flags & kScale)) { e_sum = 0; x_sum = 0; for (int i = 0; i < d.n_in; ++i) x_sum += meta[d.in_table[i]].exp2; }
             b.neg_e = (int)(-e_sum);
             // the first virtual block of the bucket publishes the output's scale exponent
             if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = x_sum;
         }
-        int64_t vid = (vb - cur_begin) * kBlock + threadIdx.x;
-        if (vid < b.n_vec) {
-            T m = eval_any<T>(b, vid);
+        const int64_t tid0 = (vb - cur_begin) * kBlock;
+        const int64_t tid = tid0 + threadIdx.x;
+        T acc[V1 * V2];
+        if (tid < b.n_tiles) {
+            T m = compute_tile<T, NIN, V1, V2>(b, tid, acc);
             lmax = m > lmax ? m : lmax;
         }
+        store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
+                                lds + (threadIdx.x >> 6) * kLdsWaveBytes);
     }
     if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
 }
 
 // One bucket whose descriptor travels in the kernel-argument segment: used by
 // the single-op API (Factor::product / sum_out / conditioning), no rescaling.
-template <typename T>
+template <typename T, int NIN, int V1, int V2>
 __global__ __launch_bounds__(kBlock) void bucket_single_kernel(const SingleArgs args) {
     // read the argument block in place (constant address space, scalar loads)
     // instead of letting the compiler copy it to scratch
@@ -284,49 +387,383 @@ __global__ __launch_bounds__(kBlock) void bucket_single_kernel(const SingleArgs 
 #endif
     const BucketDesc &d = a.d;
     LoadedBucket b;
-    b.n_in = d.n_in; b.n_dims = d.n_dims; b.k = d.k; b.vec = d.vec; b.flags = 0; b.neg_e = 0;
-    b.n_vec = d.n_vec;
-    b.dims = a.pool;
+    load_common(b, d, a.pool);
+    b.flags = 0;
+    b.neg_e = 0;
     b.out = a.meta[d.n_in].ptr;
-    for (int i = 0; i < kMaxIn; ++i) {
-        bool on = i < d.n_in;
-        b.ptr[i] = on ? a.meta[i].ptr : nullptr;
-        b.base[i] = on ? d.in_base[i] : 0;
-        b.es[i] = on ? d.elim_stride[i] : 0;
-        b.sf[i] = on && d.n_dims > 0 ? a.pool[2 + i] : 0;
+    for (int i = 0; i < kMaxIn; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : nullptr;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * kLdsWaveBytes];
+    for (int64_t tid0 = (int64_t)blockIdx.x * kBlock; tid0 < b.n_tiles; tid0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t tid = tid0 + threadIdx.x;
+        T acc[V1 * V2];
+        if (tid < b.n_tiles) (void)compute_tile<T, NIN, V1, V2>(b, tid, acc);
+        store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
+                                lds + (threadIdx.x >> 6) * kLdsWaveBytes);
     }
-    for (int64_t vid = (int64_t)blockIdx.x * kBlock + threadIdx.x; vid < b.n_vec; vid += (int64_t)gridDim.x * kBlock)
-        (void)eval_any<T>(b, vid);
+}
+
+// ------------------------------------------------------------ stream form
+// One big input streamed from HBM (its loads for 4 consecutive values of the
+// summed variable are issued before any is used; their class is a template
+// parameter, so no register shuffling sits between issue and use) and every
+// small input (factor tables, <= kStreamSmallMax entries) read from a copy in
+// LDS made once per workgroup and bucket.  Product order is still the
+// reference's chain order.
+template <typename T, int V1, int V2, int BC>
+struct BigTile {
+    static constexpr int TS = V1 * V2;
+    static constexpr int N = BC == kBigRow ? V1 : BC == kBigCol ? V2 : TS;
+    static __device__ __forceinline__ void issue(const T *src, int64_t s0, int64_t s1, T (&buf)[N]) {
+        if constexpr (BC == kBigRow) {
+            load_n<T, V1>(src, buf);
+        } else if constexpr (BC == kBigCol) {
+            load_n<T, V2>(src, buf);
+        } else if constexpr (BC == kBigFull) {
+            load_n<T, TS>(src, buf);
+        } else {
+#pragma unroll
+            for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+                for (int j1 = 0; j1 < V1; ++j1) buf[j2 * V1 + j1] = src[(int64_t)j1 * s0 + (int64_t)j2 * s1];
+        }
+    }
+    static __device__ __forceinline__ void apply(const T (&buf)[N], T (&p)[TS]) {
+#pragma unroll
+        for (int j = 0; j < TS; ++j) {
+            if constexpr (BC == kBigRow) p[j] = p[j] * buf[j % V1];
+            else if constexpr (BC == kBigCol) p[j] = p[j] * buf[j / V1];
+            else p[j] = p[j] * buf[j];
+        }
+    }
+};
+
+constexpr int kStreamMaxIn = 4;     // stream form: at most 4 inputs (planner-enforced)
+
+struct StreamState {
+    int big;
+    int32_t lds_off[kMaxIn];
+    int32_t span[kMaxIn];
+};
+
+template <typename T, int V1, int V2, int BC>
+__device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const StreamState &st, const T *small,
+                                                 int64_t tid, T (&acc)[V1 * V2]) {
+    constexpr int TS = V1 * V2;
+    using BT = BigTile<T, V1, V2, BC>;
+    int64_t pos[kStreamMaxIn];
+#pragma unroll
+    for (int i = 0; i < kStreamMaxIn; ++i) pos[i] = b.base[i];
+    if (b.n_dims > 0) {
+        uint64_t q, r;
+        divmod_dim((uint64_t)tid, b.t0h, b.t0m, q, r);
+        int64_t i0 = (int64_t)r * V1;
+#pragma unroll
+        for (int i = 0; i < kStreamMaxIn; ++i) pos[i] += i0 * b.s0[i];
+        if (b.n_dims > 1) {
+            uint64_t q1, r1;
+            divmod_dim(q, b.t1h, b.t1m, q1, r1);
+            int64_t i1 = (int64_t)r1 * V2;
+#pragma unroll
+            for (int i = 0; i < kStreamMaxIn; ++i) pos[i] += i1 * b.s1[i];
+            uint64_t rem = q1;
+            const int row = 2 + b.n_in;
+            const int64_t *dp = b.dims + 2 * row;
+            for (int j = 2; j < b.n_dims; ++j) {
+                uint64_t qq, rr;
+                divmod_dim(rem, dp[0], dp[1], qq, rr);
+#pragma unroll
+                for (int i = 0; i < kStreamMaxIn; ++i)
+                    if (i < b.n_in) pos[i] += (int64_t)rr * dp[2 + i];
+                rem = qq;
+                dp += row;
+            }
+        }
+    }
+    // LDS-relative positions of the small inputs; the big input's address and
+    // strides picked with static indices (a runtime index would go to scratch)
+    int32_t rel[kStreamMaxIn];
+    const T *bsrc = nullptr;
+    int64_t bes = 0, bs0 = 0, bs1 = 0;
+#pragma unroll
+    for (int i = 0; i < kStreamMaxIn; ++i) {
+        rel[i] = st.lds_off[i] + (int32_t)(pos[i] - b.base[i]);
+        if (i == st.big) {
+            bsrc = static_cast<const T *>(b.ptr[i]) + pos[i];
+            bes = b.es[i];
+            bs0 = b.s0[i];
+            bs1 = b.s1[i];
+        }
+    }
+
+#pragma unroll
+    for (int j = 0; j < TS; ++j) acc[j] = T(0);
+    constexpr int U = 4;
+    for (int v0 = 0; v0 < b.k; v0 += U) {
+        T bb[U][BT::N];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (v0 + u < b.k) BT::issue(bsrc + (int64_t)(v0 + u) * bes, bs0, bs1, bb[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int v = v0 + u;
+            if (v >= b.k) break;                                // uniform
+            T p[TS];
+#pragma unroll
+            for (int j = 0; j < TS; ++j) p[j] = T(1);
+#pragma unroll
+            for (int i = 0; i < kStreamMaxIn; ++i) {
+                if (i >= b.n_in) break;                         // uniform
+                if (i == st.big) {
+                    BT::apply(bb[u], p);
+                } else {
+                    const T *t = small + rel[i] + v * (int32_t)b.es[i];
+                    const int32_t s0 = (int32_t)b.s0[i], s1 = (int32_t)b.s1[i];
+#pragma unroll
+                    for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+                        for (int j1 = 0; j1 < V1; ++j1) p[j2 * V1 + j1] = p[j2 * V1 + j1] * t[j1 * s0 + j2 * s1];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < TS; ++j) acc[j] = acc[j] + p[j];
+        }
+    }
+    if (b.flags & kScale) {
+#pragma unroll
+        for (int j = 0; j < TS; ++j) acc[j] = ldexp_t(acc[j], b.neg_e);
+    }
+    T m = T(0);
+#pragma unroll
+    for (int j = 0; j < TS; ++j) m = acc[j] > m ? acc[j] : m;
+    return m;
+}
+
+// copy every small input of the bucket into LDS (uniform control flow)
+template <typename T>
+__device__ __forceinline__ void stage_small(const LoadedBucket &b, const StreamState &st, T *small) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kStreamMaxIn; ++i) {            // static indices: no scratch
+        if (i >= b.n_in) break;
+        if (i == st.big) continue;
+        const T *src = static_cast<const T *>(b.ptr[i]) + b.base[i];
+        for (int e = threadIdx.x; e < st.span[i]; e += kBlock) small[st.lds_off[i] + e] = src[e];
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void load_stream_state(StreamState &st, const BucketDesc &d) {
+    st.big = d.big;
+    for (int i = 0; i < kMaxIn; ++i) {
+        st.lds_off[i] = d.in_lds_off[i];
+        st.span[i] = d.in_span[i];
+    }
+}
+
+constexpr int kRedBytes = 64;       // block max reduction scratch at the head of dynamic LDS
+
+template <typename T, int V1, int V2, int BC>
+__global__ __launch_bounds__(kBlock) void stream_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
+                                                              const int64_t *__restrict__ pool,
+                                                              TableMeta *__restrict__ meta, int64_t total_vblocks) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    T *red = reinterpret_cast<T *>(dyn);
+    unsigned char *stage = dyn + kRedBytes;
+    T *small = reinterpret_cast<T *>(dyn + kRedBytes + (kBlock / 64) * kLdsWaveBytes);
+    LoadedBucket b;
+    StreamState st;
+    int cur = -1;
+    int64_t cur_begin = 0;
+    T lmax = T(0);
+    for (int64_t vb = blockIdx.x; vb < total_vblocks; vb += gridDim.x) {
+        int bi = n_desc == 1 ? 0 : find_bucket(descs, n_desc, vb);
+        if (bi != cur) {
+            if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
+            cur = bi;
+            lmax = T(0);
+            const BucketDesc &d = descs[bi];
+            cur_begin = d.vblk_begin;
+            load_common(b, d, pool + d.dim_off);
+            load_stream_state(st, d);
+            b.flags = d.flags;
+            b.out = meta[d.out_table].ptr;
+            int64_t e_sum = 0, x_sum = 0;
+            for (int i = 0; i < kMaxIn; ++i) {
+                if (i < d.n_in) {
+                    const TableMeta &mi = meta[d.in_table[i]];
+                    b.ptr[i] = mi.ptr;
+                    int e = FBits<T>::exponent(mi.maxbits);
+                    if (d.flags & kScale) {
+                        e_sum += e;
+                        x_sum += mi.exp2 + e;
+                    } else {
+                        x_sum += mi.exp2;
+                    }
+                } else {
+                    b.ptr[i] = nullptr;
+                }
+            }
+            b.neg_e = (int)(-e_sum);
+            if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = x_sum;
+            stage_small<T>(b, st, small);
+        }
+        const int64_t tid0 = (vb - cur_begin) * kBlock;
+        const int64_t tid = tid0 + threadIdx.x;
+        T acc[V1 * V2];
+        if (tid < b.n_tiles) {
+            T m = compute_stream_tile<T, V1, V2, BC>(b, st, small, tid, acc);
+            lmax = m > lmax ? m : lmax;
+        }
+        store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
+                                stage + (threadIdx.x >> 6) * kLdsWaveBytes);
+    }
+    if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
+}
+
+template <typename T, int V1, int V2, int BC>
+__global__ __launch_bounds__(kBlock) void stream_single_kernel(const SingleArgs args) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    (void)args;
+    const SingleArgs &a = *(const __attribute__((address_space(4))) SingleArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    const SingleArgs &a = args;
+#endif
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    unsigned char *stage = dyn + kRedBytes;
+    T *small = reinterpret_cast<T *>(dyn + kRedBytes + (kBlock / 64) * kLdsWaveBytes);
+    const BucketDesc &d = a.d;
+    LoadedBucket b;
+    StreamState st;
+    load_common(b, d, a.pool);
+    load_stream_state(st, d);
+    b.flags = 0;
+    b.neg_e = 0;
+    b.out = a.meta[d.n_in].ptr;
+    for (int i = 0; i < kMaxIn; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : nullptr;
+    stage_small<T>(b, st, small);
+    for (int64_t tid0 = (int64_t)blockIdx.x * kBlock; tid0 < b.n_tiles; tid0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t tid = tid0 + threadIdx.x;
+        T acc[V1 * V2];
+        if (tid < b.n_tiles) (void)compute_stream_tile<T, V1, V2, BC>(b, st, small, tid, acc);
+        store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
+                                stage + (threadIdx.x >> 6) * kLdsWaveBytes);
+    }
 }
 
 // ---------------------------------------------------------------- launchers
-template <typename T>
-static hipError_t launch_level_t(const BucketDesc *descs, int n_desc, const int64_t *pool, TableMeta *meta,
-                                 int64_t total_vblocks, int max_grid, hipStream_t stream) {
-    if (n_desc <= 0 || total_vblocks <= 0) return hipSuccess;
-    int64_t grid = total_vblocks < max_grid ? total_vblocks : max_grid;
-    hipLaunchKernelGGL(bucket_level_kernel<T>, dim3((unsigned)grid), dim3(kBlock), 0, stream, descs, n_desc, pool,
-                       meta, total_vblocks);
+struct LevelArgs {
+    const BucketDesc *descs;
+    int n_desc;
+    const int64_t *pool;
+    TableMeta *meta;
+    int64_t vblocks;
+};
+
+template <typename T, int NIN, int V1, int V2>
+static hipError_t go_level(const LevelArgs &a, int max_grid, hipStream_t stream) {
+    int64_t grid = a.vblocks < max_grid ? a.vblocks : max_grid;
+    hipLaunchKernelGGL((bucket_level_kernel<T, NIN, V1, V2>), dim3((unsigned)grid), dim3(kBlock), 0, stream, a.descs,
+                       a.n_desc, a.pool, a.meta, a.vblocks);
     return hipGetLastError();
 }
 
-template <typename T>
-static hipError_t launch_single_t(const SingleArgs &a, int max_grid, hipStream_t stream) {
-    int64_t blocks = (a.d.n_vec + kBlock - 1) / kBlock;
-    if (blocks <= 0) return hipSuccess;
+template <typename T, int NIN, int V1, int V2>
+static hipError_t go_single(const SingleArgs &a, int max_grid, hipStream_t stream) {
+    int64_t blocks = (a.d.n_tiles + kBlock - 1) / kBlock;
     int64_t grid = blocks < max_grid ? blocks : max_grid;
-    hipLaunchKernelGGL(bucket_single_kernel<T>, dim3((unsigned)grid), dim3(kBlock), 0, stream, a);
+    hipLaunchKernelGGL((bucket_single_kernel<T, NIN, V1, V2>), dim3((unsigned)grid), dim3(kBlock), 0, stream, a);
     return hipGetLastError();
+}
+
+template <typename T, int V1, int V2, int BC>
+static hipError_t go_stream_level(const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream) {
+    int64_t grid = a.vblocks < max_grid ? a.vblocks : max_grid;
+    size_t shm = kRedBytes + (kBlock / 64) * kLdsWaveBytes + (size_t)small_elems * sizeof(T);
+    hipLaunchKernelGGL((stream_level_kernel<T, V1, V2, BC>), dim3((unsigned)grid), dim3(kBlock), shm, stream, a.descs,
+                       a.n_desc, a.pool, a.meta, a.vblocks);
+    return hipGetLastError();
+}
+
+template <typename T, int V1, int V2, int BC>
+static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_t stream) {
+    int64_t blocks = (a.d.n_tiles + kBlock - 1) / kBlock;
+    int64_t grid = blocks < max_grid ? blocks : max_grid;
+    size_t shm = kRedBytes + (kBlock / 64) * kLdsWaveBytes + (size_t)a.d.small_elems * sizeof(T);
+    hipLaunchKernelGGL((stream_single_kernel<T, V1, V2, BC>), dim3((unsigned)grid), dim3(kBlock), shm, stream, a);
+    return hipGetLastError();
+}
+
+#define BNPP_STREAM_BC(X, T, V1, V2) X(T, V1, V2, 1) X(T, V1, V2, 2) X(T, V1, V2, 3) X(T, V1, V2, 4)
+#define BNPP_STREAM_F32(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
+    BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2) BNPP_STREAM_BC(X, T, 4, 4)
+#define BNPP_STREAM_F64(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
+    BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2)
+#define BNPP_CASE_SLEVEL(T, V1, V2, BC) \
+    case 4096 + BC * 64 + V1 * 8 + V2: return go_stream_level<T, V1, V2, BC>(a, small_elems, max_grid, stream);
+#define BNPP_CASE_SSINGLE(T, V1, V2, BC) \
+    case 4096 + BC * 64 + V1 * 8 + V2: return go_stream_single<T, V1, V2, BC>(a, max_grid, stream);
+
+static hipError_t dispatch_stream_level(bool f32, int key, const LevelArgs &a, int small_elems, int max_grid,
+                                        hipStream_t stream) {
+    if (f32) {
+        switch (key) { BNPP_STREAM_F32(BNPP_CASE_SLEVEL, float) default: break; }
+    } else {
+        switch (key) { BNPP_STREAM_F64(BNPP_CASE_SLEVEL, double) default: break; }
+    }
+    return hipErrorInvalidValue;
+}
+
+static hipError_t dispatch_stream_single(bool f32, int key, const SingleArgs &a, int max_grid, hipStream_t stream) {
+    if (f32) {
+        switch (key) { BNPP_STREAM_F32(BNPP_CASE_SSINGLE, float) default: break; }
+    } else {
+        switch (key) { BNPP_STREAM_F64(BNPP_CASE_SSINGLE, double) default: break; }
+    }
+    return hipErrorInvalidValue;
+}
+
+// every (nin class, v1, v2) the planner can produce for T
+#define BNPP_TILES_F32(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
+    X(T, NIN, 4, 2) X(T, NIN, 4, 4)
+#define BNPP_TILES_F64(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
+    X(T, NIN, 4, 2)
+#define BNPP_ALL(X, TILES, T) TILES(X, T, 1) TILES(X, T, 2) TILES(X, T, 4) TILES(X, T, 8)
+
+#define BNPP_CASE_LEVEL(T, NIN, V1, V2) \
+    case NIN * 64 + V1 * 8 + V2: return go_level<T, NIN, V1, V2>(a, max_grid, stream);
+#define BNPP_CASE_SINGLE(T, NIN, V1, V2) \
+    case NIN * 64 + V1 * 8 + V2: return go_single<T, NIN, V1, V2>(a, max_grid, stream);
+
+static hipError_t dispatch_level(bool f32, int key, const LevelArgs &a, int max_grid, hipStream_t stream) {
+    if (f32) {
+        switch (key) { BNPP_ALL(BNPP_CASE_LEVEL, BNPP_TILES_F32, float) default: break; }
+    } else {
+        switch (key) { BNPP_ALL(BNPP_CASE_LEVEL, BNPP_TILES_F64, double) default: break; }
+    }
+    return hipErrorInvalidValue;
+}
+
+static hipError_t dispatch_single(bool f32, int key, const SingleArgs &a, int max_grid, hipStream_t stream) {
+    if (f32) {
+        switch (key) { BNPP_ALL(BNPP_CASE_SINGLE, BNPP_TILES_F32, float) default: break; }
+    } else {
+        switch (key) { BNPP_ALL(BNPP_CASE_SINGLE, BNPP_TILES_F64, double) default: break; }
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream) {
-    return is_f32 ? launch_single_t<float>(a, max_grid, stream) : launch_single_t<double>(a, max_grid, stream);
+    if (a.d.n_tiles <= 0) return hipSuccess;
+    if (a.d.big >= 0) return dispatch_stream_single(is_f32 != 0, stream_key(a.d.bcls, a.d.v1, a.d.v2), a, max_grid, stream);
+    return dispatch_single(is_f32 != 0, variant_key(a.d.n_in, a.d.v1, a.d.v2), a, max_grid, stream);
 }
 
-hipError_t launch_level(int is_f32, const BucketDesc *descs, int n_desc, const int64_t *pool, TableMeta *meta,
-                        int64_t total_vblocks, int max_grid, hipStream_t stream) {
-    return is_f32 ? launch_level_t<float>(descs, n_desc, pool, meta, total_vblocks, max_grid, stream)
-                  : launch_level_t<double>(descs, n_desc, pool, meta, total_vblocks, max_grid, stream);
+hipError_t launch_level(int is_f32, int variant, const BucketDesc *descs, int n_desc, const int64_t *pool,
+                        TableMeta *meta, int64_t total_vblocks, int small_elems, int max_grid, hipStream_t stream) {
+    if (n_desc <= 0 || total_vblocks <= 0) return hipSuccess;
+    LevelArgs a{descs, n_desc, pool, meta, total_vblocks};
+    if (variant >= 4096) return dispatch_stream_level(is_f32 != 0, variant, a, small_elems, max_grid, stream);
+    return dispatch_level(is_f32 != 0, variant, a, max_grid, stream);
 }
 
 }  // namespace bnpp

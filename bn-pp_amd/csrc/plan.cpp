@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <map>
 
 namespace bnpp {
@@ -153,25 +154,38 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     k = cards[b.elim_var];
                 }
     }
-    // widest vector that divides the fastest dim and keeps stride-1 inputs aligned
-    int vec = 1;
+    // register tile: v1 entries of the fastest dim (vector loads for stride-1
+    // inputs), then v2 entries of the next dim when v1 covers the whole fastest
+    // dim (the tile is then v1*v2 contiguous output entries)
+    int max_tile = max_vec == 2 ? 8 : 16;
+    if (const char *e = std::getenv("BNPP_MAX_TILE")) max_tile = std::max(1, std::min(max_tile, std::atoi(e)));
+    auto aligned = [&](int dim, int v) {
+        for (int i = 0; i < n; ++i) {
+            if (merged[dim].s[i] != 1) continue;
+            bool lower_zero = true;           // stride-1 on `dim`, absent on faster dims
+            for (int j = 0; j < dim; ++j)
+                if (merged[j].s[i] != 0) lower_zero = false;
+            if (!lower_zero) continue;
+            if (b.in[i].base % v || es[i] % v) return false;
+            for (size_t j = dim + 1; j < merged.size(); ++j)
+                if (merged[j].s[i] % v) return false;
+        }
+        return true;
+    };
+    int v1 = 1, v2 = 1;
     if (!merged.empty()) {
-        for (int v = max_vec; v >= 2; v >>= 1) {
-            if (merged[0].card % (uint64_t)v) continue;
-            bool ok = true;
-            for (int i = 0; ok && i < n; ++i) {
-                if (merged[0].s[i] != 1) continue;
-                if (b.in[i].base % v || es[i] % v) ok = false;
-                for (size_t j = 1; ok && j < merged.size(); ++j)
-                    if (merged[j].s[i] % v) ok = false;
-            }
-            if (ok) { vec = v; break; }
+        for (int v = 4; v >= 2; v >>= 1)
+            if (v <= max_tile && merged[0].card % (uint64_t)v == 0 && aligned(0, v)) { v1 = v; break; }
+        if (merged.size() >= 2 && (uint64_t)v1 == merged[0].card) {
+            for (int v = max_tile / v1; v >= 2; v >>= 1)
+                if (v <= 4 && merged[1].card % (uint64_t)v == 0 && aligned(1, v)) { v2 = v; break; }
         }
     }
     d = BucketDesc{};
     d.out_size = out_size;
-    d.vec = vec;
-    d.n_vec = out_size / vec;
+    d.v1 = v1;
+    d.v2 = v2;
+    d.n_tiles = out_size / (v1 * v2);
     d.n_in = n;
     d.n_dims = (int)merged.size();
     d.k = k;
@@ -181,6 +195,50 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         d.in_table[i] = i < n ? b.in[i].table : 0;
         d.in_base[i] = i < n ? b.in[i].base : 0;
         d.elim_stride[i] = es[i];
+    }
+    auto divisor = [&](uint64_t c, int64_t *hdr) {
+        uint32_t shift, magic;
+        bool pow2;
+        magic_for((uint32_t)c, shift, magic, pow2);
+        hdr[0] = pack_dim_header((uint32_t)c, shift, pow2);
+        hdr[1] = (int64_t)magic;
+    };
+    divisor(merged.empty() ? 1 : merged[0].card / v1, d.tdiv0);
+    divisor(merged.size() < 2 ? 1 : merged[1].card / v2, d.tdiv1);
+    // stream form: exactly one input too big for LDS, the rest small enough
+    d.big = -1;
+    {
+        int big = -1, n_big = 0;
+        int64_t small_total = 0;
+        int64_t span[kMaxIn];
+        for (int i = 0; i < n; ++i) {
+            int64_t sp = 1 + es[i] * (k - 1);
+            for (size_t j = 0; j < b.in[i].vars.size(); ++j)
+                if (b.in[i].vars[j] != b.elim_var) sp += (int64_t)(cards[b.in[i].vars[j]] - 1) * b.in[i].strides[j];
+            span[i] = sp;
+            if (sp > kStreamSmallMax) { big = i; ++n_big; }
+            else small_total += sp;
+        }
+        const int eb = max_vec == 2 ? 8 : 4;
+        const char *off = std::getenv("BNPP_NO_STREAM");
+        if (n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 && !(off && *off == '1')) {
+            int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
+            int64_t s1 = merged.size() < 2 ? 0 : merged[1].s[big];
+            int bc;
+            if (v1 > 1 && s0 == 1 && (v2 == 1 || s1 == 0)) bc = kBigRow;
+            else if (v2 > 1 && s0 == 0 && s1 == 1) bc = kBigCol;
+            else if (v1 > 1 && v2 > 1 && s0 == 1 && s1 == v1) bc = kBigFull;
+            else bc = kBigDirect;
+            d.big = big;
+            d.bcls = bc;
+            int32_t o = 0;
+            for (int i = 0; i < n; ++i) {
+                d.in_span[i] = (int32_t)span[i];
+                d.in_lds_off[i] = i == big ? 0 : o;
+                if (i != big) o += (int32_t)((span[i] + 3) & ~3);       // keep 16-B alignment
+            }
+            d.small_elems = o;
+        }
     }
     d.dim_off = (int64_t)pool.size();
     for (const Dim &dm : merged) {
@@ -414,21 +472,33 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     for (size_t pi = 0; pi < plans.size(); ++pi)
         for (const BucketSpec &b : plans[pi]->buckets) by_level[b.level].push_back({pi, &b});
     for (int L = 1; L <= n_levels; ++L) {
-        s.level_begin.push_back((int)s.descs.size());
-        int64_t vb = 0;
+        std::vector<std::pair<int, BucketDesc>> lv;
         for (auto &pb : by_level[L]) {
             BucketSpec b = *pb.second;
             for (View &v : b.in) v.table = remap(pb.first, v.table);
             b.out_table = remap(pb.first, b.out_table);
             BucketDesc d;
             if (!build_desc(b, cards, max_vec, d, s.pool, msg)) return false;
-            d.vblk_begin = vb;
-            vb += (d.n_vec + kBlock - 1) / kBlock;
-            s.descs.push_back(d);
+            lv.push_back({d.big >= 0 ? stream_key(d.bcls, d.v1, d.v2) : variant_key(d.n_in, d.v1, d.v2), d});
         }
-        s.level_vblocks.push_back(vb);
+        std::stable_sort(lv.begin(), lv.end(), [](const std::pair<int, BucketDesc> &a,
+                                                  const std::pair<int, BucketDesc> &b) { return a.first < b.first; });
+        for (size_t i = 0; i < lv.size();) {
+            Schedule::Group g{L, lv[i].first, (int)s.descs.size(), 0, 0, 0};
+            int64_t vb = 0;
+            for (; i < lv.size() && lv[i].first == g.variant; ++i) {
+                BucketDesc d = lv[i].second;
+                g.small_elems = std::max(g.small_elems, d.big >= 0 ? d.small_elems : 0);
+                d.vblk_begin = vb;
+                vb += (d.n_tiles + kBlock - 1) / kBlock;
+                s.descs.push_back(d);
+            }
+            g.end = (int)s.descs.size();
+            g.vblocks = vb;
+            s.groups.push_back(g);
+        }
     }
-    s.level_begin.push_back((int)s.descs.size());
+    s.n_levels = n_levels;
     return true;
 }
 

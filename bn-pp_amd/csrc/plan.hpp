@@ -80,8 +80,13 @@ struct Schedule {
     std::vector<int64_t> table_offset;      // bytes into the arena (messages only; -1 for sources)
     std::vector<BucketDesc> descs;          // grouped by level, vblk_begin relative to the level
     std::vector<int64_t> pool;
-    std::vector<int> level_begin;           // descs index where each level starts (+ end sentinel)
-    std::vector<int64_t> level_vblocks;     // virtual blocks per level
+    struct Group {                          // one launch: buckets of one level and one kernel variant
+        int level, variant, begin, end;
+        int64_t vblocks;
+        int small_elems;                    // stream kernels: LDS elements for small inputs
+    };
+    std::vector<Group> groups;
+    int n_levels = 0;
     std::vector<int> plan_result_table;     // per plan (-1: constant 1)
     std::vector<std::vector<int>> plan_result_vars;
     int64_t arena_bytes = 0;

@@ -121,11 +121,9 @@ int launch(Context &ctx, Executable &ex, hipStream_t stream) {
     hipError_t err = hipMemcpyAsync(ex.d_meta, ex.d_meta0, sizeof(TableMeta) * (size_t)sc.n_tables,
                                     hipMemcpyDeviceToDevice, stream);
     if (err != hipSuccess) return fail(ctx, err, "hipMemcpyAsync(meta reset)");
-    const int n_levels = (int)sc.level_vblocks.size();
-    for (int L = 0; L < n_levels; ++L) {
-        int b0 = sc.level_begin[L], b1 = sc.level_begin[L + 1];
-        err = launch_level(ex.dtype == kF32, ex.d_desc + b0, b1 - b0, ex.d_pool, ex.d_meta, sc.level_vblocks[L],
-                           ctx.max_grid, stream);
+    for (const Schedule::Group &g : sc.groups) {
+        err = launch_level(ex.dtype == kF32, g.variant, ex.d_desc + g.begin, g.end - g.begin, ex.d_pool, ex.d_meta,
+                           g.vblocks, g.small_elems, ctx.max_grid, stream);
         if (err != hipSuccess) return fail(ctx, err, "launch_level");
     }
     return 0;

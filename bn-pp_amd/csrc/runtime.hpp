@@ -12,8 +12,8 @@
 
 namespace bnpp {
 
-hipError_t launch_level(int is_f32, const BucketDesc *descs, int n_desc, const int64_t *pool, TableMeta *meta,
-                        int64_t total_vblocks, int max_grid, hipStream_t stream);
+hipError_t launch_level(int is_f32, int variant, const BucketDesc *descs, int n_desc, const int64_t *pool,
+                        TableMeta *meta, int64_t total_vblocks, int small_elems, int max_grid, hipStream_t stream);
 
 // single bucket with the descriptor passed by value (no device-side metadata,
 // no rescaling): the exact Factor::product / sum_out / conditioning semantics.

@@ -25,8 +25,18 @@ DEV = "cuda"
 TD = {bnpp.F64: torch.float64, bnpp.F32: torch.float32}
 
 
+_STREAM = None
+
+
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    """A dedicated non-null torch stream shared by the tests' torch ops and the
+    engine's launches (torch's default stream handle is 0, which the ABI reads
+    as 'the context stream')."""
+    global _STREAM
+    if _STREAM is None:
+        _STREAM = torch.cuda.Stream()
+    torch.cuda.set_stream(_STREAM)
+    return _STREAM.cuda_stream
 
 
 def _dev(vals, dtype):
