@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -30,7 +31,7 @@ struct bnpp_job {
     bnpp_ctx *ctx = nullptr;
     int kind = 0;
     DeviceSources src;
-    Executable ex;
+    Program pg;
     std::vector<int> targets;
     std::vector<int> ev_val;          // per variable, -1 = no evidence
     std::vector<int> cards;
@@ -183,29 +184,64 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
     return BNPP_OK;
 }
 
-int plan_schedule(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
-                  int n_order, const std::vector<int> &targets, int dtype, Schedule &s, double *stats) {
+// Plans -> schedules.  MAR targets are split into batches whose estimated
+// arenas fit `budget` bytes; a batch runs as one level-aligned schedule.
+int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
+                   int n_order, const std::vector<int> &targets, int dtype, int64_t budget,
+                   std::vector<Schedule> &out, double *stats) {
     std::vector<VEPlan> plans;
     int width = 0;
     int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width);
     if (rc) return rc;
-    std::vector<const VEPlan *> pp;
-    for (auto &p : plans) pp.push_back(&p);
+    const int eb = dtype == BNPP_F32 ? 4 : 8;
     std::vector<int64_t> src_sizes;
     for (auto &v : d.values) src_sizes.push_back((int64_t)v.size());
-    const int eb = dtype == BNPP_F32 ? 4 : 8;
+    std::vector<std::vector<const VEPlan *>> batches(1);
+    int64_t acc = 0;
+    for (auto &p : plans) {
+        int64_t need = plan_peak_bytes(p, eb) + (int64_t)p.buckets.size() * 512;
+        if (!batches.back().empty() && acc + need > budget) {
+            batches.emplace_back();
+            acc = 0;
+        }
+        batches.back().push_back(&p);
+        acc += need;
+    }
+    out.clear();
     std::string msg;
-    if (!build_schedule(pp, d.cards, src_sizes, eb, max_vec_for(dtype), s, &msg)) return set_err(BNPP_ERR_INVALID, msg);
-    stats[0] = s.entries;
-    stats[1] = (double)s.arena_bytes;
-    stats[2] = (double)s.n_levels;
-    stats[3] = (double)s.descs.size();
+    double entries = 0, moved = 0, arena = 0, levels = 0, buckets = 0;
+    for (auto &bp : batches) {
+        Schedule s;
+        if (!build_schedule(bp, d.cards, src_sizes, eb, max_vec_for(dtype), s, &msg))
+            return set_err(BNPP_ERR_INVALID, msg);
+        entries += s.entries;
+        moved += s.elems_moved;
+        arena = std::max(arena, (double)s.arena_bytes);
+        levels += s.n_levels;
+        buckets += (double)s.descs.size();
+        out.push_back(std::move(s));
+    }
+    stats[0] = entries;
+    stats[1] = arena;
+    stats[2] = levels;
+    stats[3] = buckets;
     stats[4] = width;
     int64_t mx = 0;
     for (auto &p : plans) mx = std::max(mx, p.max_table);
     stats[5] = (double)mx;
-    stats[6] = s.elems_moved * eb;
+    stats[6] = moved * eb;
+    stats[7] = (double)out.size();
     return BNPP_OK;
+}
+
+int64_t memory_budget(bnpp_ctx *ctx) {
+    if (const char *e = std::getenv("BNPP_MEM_BUDGET_GB")) return (int64_t)(std::atof(e) * 1e9);
+    if (ctx) {
+        size_t fr = 0, tot = 0;
+        (void)hipSetDevice(ctx->c.device);
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) return (int64_t)(fr * 0.6);
+    }
+    return (int64_t)64e9;
 }
 
 int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals,
@@ -230,12 +266,13 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
             for (int v = 0; v < (int)d.cards.size(); ++v) job->targets.push_back(v);
         }
     }
-    Schedule s;
-    int rc = plan_schedule(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, s, job->stats);
+    std::vector<Schedule> batches;
+    int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, memory_budget(ctx),
+                            batches, job->stats);
     if (rc) return rc;
     rc = upload_sources(ctx->c, d.values, dtype == BNPP_F32 ? kF32 : kF64, job->src);
     if (rc) return from_ctx(ctx, rc);
-    rc = make_executable(ctx->c, job->src, std::move(s), job->ex);
+    rc = make_program(ctx->c, job->src, std::move(batches), job->pg);
     if (rc) return from_ctx(ctx, rc);
     return BNPP_OK;
 }
@@ -243,7 +280,7 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
 void destroy_job(bnpp_job *job) {
     if (!job) return;
     (void)hipSetDevice(job->ctx->c.device);
-    free_executable(job->ex);
+    free_program(job->pg);
     free_sources(job->src);
     delete job;
 }
@@ -253,8 +290,11 @@ void destroy_job(bnpp_job *job) {
 int job_results(bnpp_job *job, hipStream_t stream, double *out, double *z_out) {
     std::vector<std::vector<double>> vals;
     std::vector<int64_t> exp2;
-    int rc = fetch_results(job->ctx->c, job->ex, stream, vals, exp2);
+    int rc = fetch_program(job->ctx->c, job->pg, stream, vals, exp2);
     if (rc) return from_ctx(job->ctx, rc);
+    std::vector<const std::vector<int> *> rvars;
+    for (auto &ex : job->pg.parts)
+        for (auto &v : ex.sched.plan_result_vars) rvars.push_back(&v);
     if (job->kind == 0) {
         double p = 0;                                   // part.partition(): sequential sum
         for (double v : vals[0]) p += v;
@@ -269,7 +309,7 @@ int job_results(bnpp_job *job, hipStream_t stream, double *out, double *z_out) {
         const std::vector<double> &r = vals[i];
         if (job->ev_val[t] >= 0) {                      // evidence variable: one-hot
             for (int s = 0; s < k; ++s) out[o + s] = s == job->ev_val[t] ? 1.0 : 0.0;
-        } else if ((int)r.size() == k && k > 0 && job->ex.sched.plan_result_vars[i].size() == 1) {
+        } else if ((int)r.size() == k && k > 0 && rvars[i]->size() == 1) {
             double part = 0;                            // Factor::normalize (factor.cpp:244-255)
             for (double v : r) part += v;
             for (int s = 0; s < k; ++s) out[o + s] = r[s] / part;
@@ -606,12 +646,12 @@ int bnpp_variable_elimination(bnpp_ctx *ctx, const bnpp_model *m, int n_vars, co
     if (!out_ndims || !out_size || !exp2 || (n_vars > 0 && !vars)) return set_err(BNPP_ERR_INVALID, "null argument");
     std::unique_ptr<bnpp_job> job;
     int rc = create_job(ctx, m, 2, 0, nullptr, nullptr, heuristic, vars, n_vars, 0, nullptr, dtype, job);
-    if (rc == BNPP_OK) rc = from_ctx(ctx, launch(ctx->c, job->ex, ctx->c.stream));
+    if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     std::vector<std::vector<double>> vals;
     std::vector<int64_t> e2;
-    if (rc == BNPP_OK) rc = from_ctx(ctx, fetch_results(ctx->c, job->ex, ctx->c.stream, vals, e2));
+    if (rc == BNPP_OK) rc = from_ctx(ctx, fetch_program(ctx->c, job->pg, ctx->c.stream, vals, e2));
     if (rc == BNPP_OK) {
-        const std::vector<int> &rv = job->ex.sched.plan_result_vars[0];
+        const std::vector<int> &rv = job->pg.parts[0].sched.plan_result_vars[0];
         *out_ndims = (int)rv.size();
         *out_size = (int64_t)vals[0].size();
         *exp2 = e2[0];
@@ -628,7 +668,7 @@ int bnpp_variable_elimination(bnpp_ctx *ctx, const bnpp_model *m, int n_vars, co
 }
 
 int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
-                    int dtype, double *stats, int n_stats) {
+                    const int *order, int n_order, int dtype, double *stats, int n_stats) {
     BNPP_GUARD_BEGIN
     if (!m || !stats) return set_err(BNPP_ERR_INVALID, "null argument");
     if (kind != 0 && kind != 1) return set_err(BNPP_ERR_INVALID, "kind must be 0 or 1");
@@ -637,9 +677,9 @@ int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars,
     if (!evidence_array(m->d, n_ev, ev_vars, ev_vals, ev, msg)) return set_err(BNPP_ERR_INVALID, msg);
     if (kind == 1)
         for (int v = 0; v < (int)m->d.cards.size(); ++v) targets.push_back(v);
-    Schedule s;
+    std::vector<Schedule> batches;
     double st[8] = {0};
-    int rc = plan_schedule(m->d, ev, kind, heuristic, nullptr, 0, targets, dtype, s, st);
+    int rc = plan_schedules(m->d, ev, kind, heuristic, order, n_order, targets, dtype, memory_budget(nullptr), batches, st);
     if (rc) return rc;
     for (int i = 0; i < n_stats && i < 8; ++i) stats[i] = st[i];
     return BNPP_OK;
@@ -656,7 +696,7 @@ int bnpp_job_launch(bnpp_job *job, void *stream) {
     BNPP_GUARD_BEGIN
     if (!job) return set_err(BNPP_ERR_INVALID, "null job");
     (void)hipSetDevice(job->ctx->c.device);
-    return from_ctx(job->ctx, launch(job->ctx->c, job->ex, pick_stream(job->ctx, stream)));
+    return from_ctx(job->ctx, launch_program(job->ctx->c, job->pg, pick_stream(job->ctx, stream)));
     BNPP_GUARD_END
 }
 
@@ -680,7 +720,7 @@ int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     double t0 = now_ms();
     std::unique_ptr<bnpp_job> job;
     int rc = create_job(ctx, m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype, job);
-    if (rc == BNPP_OK) rc = from_ctx(ctx, launch(ctx->c, job->ex, ctx->c.stream));
+    if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     double lz = 0, zz = 0;
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, &lz, &zz);
     if (job) destroy_job(job.release());
@@ -699,7 +739,7 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     double t0 = now_ms();
     std::unique_ptr<bnpp_job> job;
     int rc = create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, job);
-    if (rc == BNPP_OK) rc = from_ctx(ctx, launch(ctx->c, job->ex, ctx->c.stream));
+    if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
     if (job) destroy_job(job.release());
     if (rc) return rc;

@@ -516,12 +516,31 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
                 if (i == st.big) {
                     BT::apply(bb[u], p);
                 } else {
+                    // small input from LDS, read once per distinct entry of the tile
                     const T *t = small + rel[i] + v * (int32_t)b.es[i];
                     const int32_t s0 = (int32_t)b.s0[i], s1 = (int32_t)b.s1[i];
+                    if (s0 == 0 && s1 == 0) {
+                        const T y = t[0];
 #pragma unroll
-                    for (int j2 = 0; j2 < V2; ++j2)
+                        for (int j = 0; j < TS; ++j) p[j] = p[j] * y;
+                    } else if (s1 == 0) {
+                        T y[V1];
 #pragma unroll
-                        for (int j1 = 0; j1 < V1; ++j1) p[j2 * V1 + j1] = p[j2 * V1 + j1] * t[j1 * s0 + j2 * s1];
+                        for (int j1 = 0; j1 < V1; ++j1) y[j1] = t[j1 * s0];
+#pragma unroll
+                        for (int j = 0; j < TS; ++j) p[j] = p[j] * y[j % V1];
+                    } else if (s0 == 0) {
+                        T y[V2];
+#pragma unroll
+                        for (int j2 = 0; j2 < V2; ++j2) y[j2] = t[j2 * s1];
+#pragma unroll
+                        for (int j = 0; j < TS; ++j) p[j] = p[j] * y[j / V1];
+                    } else {
+#pragma unroll
+                        for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+                            for (int j1 = 0; j1 < V1; ++j1) p[j2 * V1 + j1] = p[j2 * V1 + j1] * t[j1 * s0 + j2 * s1];
+                    }
                 }
             }
 #pragma unroll
@@ -695,7 +714,8 @@ static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_
 
 #define BNPP_STREAM_BC(X, T, V1, V2) X(T, V1, V2, 1) X(T, V1, V2, 2) X(T, V1, V2, 3) X(T, V1, V2, 4)
 #define BNPP_STREAM_F32(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
-    BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2) BNPP_STREAM_BC(X, T, 4, 4)
+    BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2) BNPP_STREAM_BC(X, T, 4, 4) \
+    BNPP_STREAM_BC(X, T, 2, 8)
 #define BNPP_STREAM_F64(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
     BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2)
 #define BNPP_CASE_SLEVEL(T, V1, V2, BC) \
@@ -724,7 +744,7 @@ static hipError_t dispatch_stream_single(bool f32, int key, const SingleArgs &a,
 
 // every (nin class, v1, v2) the planner can produce for T
 #define BNPP_TILES_F32(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
-    X(T, NIN, 4, 2) X(T, NIN, 4, 4)
+    X(T, NIN, 4, 2) X(T, NIN, 4, 4) X(T, NIN, 2, 8)
 #define BNPP_TILES_F64(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
     X(T, NIN, 4, 2)
 #define BNPP_ALL(X, TILES, T) TILES(X, T, 1) TILES(X, T, 2) TILES(X, T, 4) TILES(X, T, 8)

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 
@@ -177,8 +178,9 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         for (int v = 4; v >= 2; v >>= 1)
             if (v <= max_tile && merged[0].card % (uint64_t)v == 0 && aligned(0, v)) { v1 = v; break; }
         if (merged.size() >= 2 && (uint64_t)v1 == merged[0].card) {
+            const int v2_max = (v1 == 2 && max_tile == 16) ? 8 : 4;   // instantiated tiles (kernels.hip)
             for (int v = max_tile / v1; v >= 2; v >>= 1)
-                if (v <= 4 && merged[1].card % (uint64_t)v == 0 && aligned(1, v)) { v2 = v; break; }
+                if (v <= v2_max && merged[1].card % (uint64_t)v == 0 && aligned(1, v)) { v2 = v; break; }
         }
     }
     d = BucketDesc{};
@@ -367,6 +369,28 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
     return p;
 }
 
+int64_t plan_peak_bytes(const VEPlan &p, int elem_bytes) {
+    const int nt = p.n_src + (int)p.msgs.size();
+    std::vector<int> born(nt, 0), last(nt, -1);
+    for (const BucketSpec &b : p.buckets) {
+        born[b.out_table] = b.level;
+        for (const View &v : b.in) last[v.table] = std::max(last[v.table], b.level);
+    }
+    if (p.result_table >= 0) last[p.result_table] = p.n_levels + 1;
+    std::vector<int64_t> delta(p.n_levels + 3, 0);
+    for (int t = p.n_src; t < nt; ++t) {
+        int64_t bytes = ((p.msgs[t - p.n_src].size * elem_bytes + 255) / 256) * 256;
+        delta[born[t]] += bytes;
+        delta[std::max(last[t], born[t]) + 1] -= bytes;
+    }
+    int64_t live = 0, peak = 0;
+    for (int64_t d : delta) {
+        live += d;
+        peak = std::max(peak, live);
+    }
+    return peak;
+}
+
 // ------------------------------------------------------------- schedule
 namespace {
 struct Arena {
@@ -483,6 +507,22 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         }
         std::stable_sort(lv.begin(), lv.end(), [](const std::pair<int, BucketDesc> &a,
                                                   const std::pair<int, BucketDesc> &b) { return a.first < b.first; });
+        if (std::getenv("BNPP_DUMP_PLAN")) {
+            for (auto &e : lv) {
+                const BucketDesc &d = e.second;
+                std::fprintf(stderr, "L%d n_in=%d k=%d tile=%dx%d big=%d bcls=%d tiles=%lld dims:", L, d.n_in, d.k, d.v1,
+                             d.v2, d.big, d.big >= 0 ? d.bcls : 0, (long long)d.n_tiles);
+                for (int j = 0; j < d.n_dims; ++j) {
+                    const int64_t *row = s.pool.data() + d.dim_off + (int64_t)j * (2 + d.n_in);
+                    std::fprintf(stderr, " [%u:", (unsigned)((uint64_t)row[0] & 0xffffffffu));
+                    for (int i = 0; i < d.n_in; ++i) std::fprintf(stderr, "%s%lld", i ? "," : "", (long long)row[2 + i]);
+                    std::fprintf(stderr, "]");
+                }
+                std::fprintf(stderr, " es:");
+                for (int i = 0; i < d.n_in; ++i) std::fprintf(stderr, "%s%lld", i ? "," : "", (long long)d.elim_stride[i]);
+                std::fprintf(stderr, "\n");
+            }
+        }
         for (size_t i = 0; i < lv.size();) {
             Schedule::Group g{L, lv[i].first, (int)s.descs.size(), 0, 0, 0};
             int64_t vb = 0;

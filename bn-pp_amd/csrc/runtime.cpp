@@ -1,6 +1,7 @@
 // Device runtime: source upload, executable schedules, launches, result fetch.
 #include "runtime.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -72,7 +73,7 @@ void free_sources(DeviceSources &s) {
     s = DeviceSources{};
 }
 
-int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex) {
+int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex, void *shared_arena) {
     ex = Executable{};
     ex.dtype = src.dtype;
     ex.sched = std::move(s);
@@ -83,8 +84,13 @@ int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Execut
         ctx.last_error = "schedule/source count mismatch";
         return -1;
     }
-    err = hipMalloc(&ex.arena, sc.arena_bytes > 0 ? (size_t)sc.arena_bytes : 256);
-    if (err != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
+    if (shared_arena) {
+        ex.arena = shared_arena;
+        ex.own_arena = false;
+    } else {
+        err = hipMalloc(&ex.arena, sc.arena_bytes > 0 ? (size_t)sc.arena_bytes : 256);
+        if (err != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
+    }
     ex.h_meta.resize(sc.n_tables);
     for (int t = 0; t < sc.n_tables; ++t) {
         if (t < sc.n_src) {
@@ -166,12 +172,113 @@ int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<
 }
 
 void free_executable(Executable &ex) {
-    if (ex.arena) (void)hipFree(ex.arena);
+    if (ex.arena && ex.own_arena) (void)hipFree(ex.arena);
     if (ex.d_meta) (void)hipFree(ex.d_meta);
     if (ex.d_meta0) (void)hipFree(ex.d_meta0);
     if (ex.d_desc) (void)hipFree(ex.d_desc);
     if (ex.d_pool) (void)hipFree(ex.d_pool);
     ex = Executable{};
+}
+
+int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg) {
+    pg = Program{};
+    pg.dtype = src.dtype;
+    const int64_t eb = src.dtype == kF32 ? 4 : 8;
+    for (const Schedule &s : batches) pg.arena_bytes = std::max(pg.arena_bytes, s.arena_bytes);
+    hipError_t err = hipSetDevice(ctx.device);
+    if (err != hipSuccess) return fail(ctx, err, "hipSetDevice");
+    if ((err = hipMalloc(&pg.arena, pg.arena_bytes > 0 ? (size_t)pg.arena_bytes : 256)) != hipSuccess)
+        return fail(ctx, err, "hipMalloc(arena)");
+    for (const Schedule &s : batches) {
+        std::vector<int64_t> off, sz;
+        for (int t : s.plan_result_table) {
+            if (t < 0) {
+                off.push_back(-1);
+                sz.push_back(1);
+            } else {
+                off.push_back(pg.results_bytes);
+                sz.push_back(s.table_size[t]);
+                pg.results_bytes += ((s.table_size[t] * eb + 255) / 256) * 256;
+            }
+        }
+        pg.res_off.push_back(off);
+        pg.res_size.push_back(sz);
+    }
+    if ((err = hipMalloc(&pg.results, pg.results_bytes > 0 ? (size_t)pg.results_bytes : 256)) != hipSuccess)
+        return fail(ctx, err, "hipMalloc(results)");
+    pg.parts.resize(batches.size());
+    for (size_t b = 0; b < batches.size(); ++b) {
+        int rc = make_executable(ctx, src, std::move(batches[b]), pg.parts[b], pg.arena);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int launch_program(Context &ctx, Program &pg, hipStream_t stream) {
+    const int64_t eb = pg.dtype == kF32 ? 4 : 8;
+    for (size_t b = 0; b < pg.parts.size(); ++b) {
+        Executable &ex = pg.parts[b];
+        int rc = launch(ctx, ex, stream);
+        if (rc) return rc;
+        for (size_t p = 0; p < ex.sched.plan_result_table.size(); ++p) {
+            int t = ex.sched.plan_result_table[p];
+            if (t < 0) continue;
+            hipError_t err = hipMemcpyAsync(static_cast<unsigned char *>(pg.results) + pg.res_off[b][p],
+                                            ex.h_meta[t].ptr, (size_t)(ex.sched.table_size[t] * eb),
+                                            hipMemcpyDeviceToDevice, stream);
+            if (err != hipSuccess) return fail(ctx, err, "hipMemcpyAsync(result)");
+        }
+    }
+    return 0;
+}
+
+int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std::vector<double>> &vals,
+                  std::vector<int64_t> &exp2) {
+    hipError_t err = hipStreamSynchronize(stream);
+    if (err != hipSuccess) return fail(ctx, err, "hipStreamSynchronize");
+    const int64_t eb = pg.dtype == kF32 ? 4 : 8;
+    std::vector<unsigned char> raw((size_t)std::max<int64_t>(pg.results_bytes, 1));
+    if (pg.results_bytes > 0 &&
+        (err = hipMemcpy(raw.data(), pg.results, (size_t)pg.results_bytes, hipMemcpyDeviceToHost)) != hipSuccess)
+        return fail(ctx, err, "hipMemcpy(results)");
+    vals.clear();
+    exp2.clear();
+    for (size_t b = 0; b < pg.parts.size(); ++b) {
+        Executable &ex = pg.parts[b];
+        std::vector<TableMeta> meta(ex.sched.n_tables);
+        if (!meta.empty() &&
+            (err = hipMemcpy(meta.data(), ex.d_meta, sizeof(TableMeta) * meta.size(), hipMemcpyDeviceToHost)) != hipSuccess)
+            return fail(ctx, err, "hipMemcpy(meta)");
+        for (size_t p = 0; p < ex.sched.plan_result_table.size(); ++p) {
+            int t = ex.sched.plan_result_table[p];
+            if (t < 0) {
+                vals.push_back({1.0});
+                exp2.push_back(0);
+                continue;
+            }
+            std::vector<double> v((size_t)pg.res_size[b][p]);
+            const unsigned char *src = raw.data() + pg.res_off[b][p];
+            for (size_t j = 0; j < v.size(); ++j) {
+                if (eb == 4) {
+                    float x;
+                    std::memcpy(&x, src + j * 4, 4);
+                    v[j] = x;
+                } else {
+                    std::memcpy(&v[j], src + j * 8, 8);
+                }
+            }
+            vals.push_back(std::move(v));
+            exp2.push_back(meta[t].exp2);
+        }
+    }
+    return 0;
+}
+
+void free_program(Program &pg) {
+    for (Executable &ex : pg.parts) free_executable(ex);
+    if (pg.arena) (void)hipFree(pg.arena);
+    if (pg.results) (void)hipFree(pg.results);
+    pg = Program{};
 }
 
 }  // namespace bnpp

@@ -46,6 +46,7 @@ struct DeviceSources {
 // A schedule bound to device buffers, launchable many times.
 struct Executable {
     DType dtype = kF64;
+    bool own_arena = true;
     Schedule sched;
     void *arena = nullptr;
     TableMeta *d_meta = nullptr;        // live metadata
@@ -55,13 +56,34 @@ struct Executable {
     std::vector<TableMeta> h_meta;
 };
 
+// Several schedules (target batches of one MAR job) run back to back in one
+// shared arena; each batch's result tables are copied into a persistent
+// results buffer before the next batch reuses the arena.
+struct Program {
+    DType dtype = kF64;
+    std::vector<Executable> parts;
+    void *arena = nullptr;
+    int64_t arena_bytes = 0;
+    void *results = nullptr;
+    int64_t results_bytes = 0;
+    std::vector<std::vector<int64_t>> res_off;    // per part, per plan: byte offset (-1: constant 1)
+    std::vector<std::vector<int64_t>> res_size;   // per part, per plan: entries
+};
+
 int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out);
 void free_sources(DeviceSources &s);
-int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex);
+int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex, void *shared_arena = nullptr);
 int launch(Context &ctx, Executable &ex, hipStream_t stream);
 // waits for `stream`, downloads result tables: values as stored (double) and the exp2 scale
 int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<std::vector<double>> &vals,
                   std::vector<int64_t> &exp2);
 void free_executable(Executable &ex);
+
+int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg);
+int launch_program(Context &ctx, Program &pg, hipStream_t stream);
+// result values (as stored, double) and exp2 of every plan, batches in order
+int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std::vector<double>> &vals,
+                  std::vector<int64_t> &exp2);
+void free_program(Program &pg);
 
 }  // namespace bnpp

@@ -57,7 +57,7 @@ _SIGS = {
     "bnpp_marginals": (_I, [_P, _P, _I, _IP, _IP, _I, _I, _IP, _I, _DP, _DP]),
     "bnpp_variable_elimination": (_I, [_P, _P, _I, _IP, _I, _I, _I, _IP, _IP, C.c_int64, C.POINTER(C.c_int64), _DP,
                                        C.POINTER(C.c_int64)]),
-    "bnpp_plan_stats": (_I, [_P, _I, _I, _IP, _IP, _I, _I, _DP, _I]),
+    "bnpp_plan_stats": (_I, [_P, _I, _I, _IP, _IP, _I, _IP, _I, _I, _DP, _I]),
     "bnpp_job_create": (_I, [_P, _P, _I, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, C.POINTER(_P)]),
     "bnpp_job_stats": (_I, [_P, _DP, _I]),
     "bnpp_job_launch": (_I, [_P, _P]),
@@ -214,11 +214,14 @@ def out_scope(scopes: Sequence[Sequence[int]], elim: int = -1) -> List[int]:
     return list(out[: n.value])
 
 
-def plan_stats(model: Model, kind: int = 0, evidence=None, heuristic: str = "mf", dtype: int = F64) -> List[float]:
+def plan_stats(model: Model, kind: int = 0, evidence=None, heuristic: str = "mf", dtype: int = F64,
+               order: Optional[Sequence[int]] = None) -> List[float]:
     n, ev_v, ev_x = _ev(evidence)
     st = (C.c_double * 8)()
-    _check(_lib.bnpp_plan_stats(model.handle, kind, n, ev_v, ev_x, HEURISTICS[heuristic], dtype, st, 8),
-           "bnpp_plan_stats")
+    oa = _ints(order) if order is not None else None
+    h = ORDER_GIVEN if order is not None else HEURISTICS[heuristic]
+    _check(_lib.bnpp_plan_stats(model.handle, kind, n, ev_v, ev_x, h, oa, len(order) if order is not None else 0,
+                                dtype, st, 8), "bnpp_plan_stats")
     return list(st)
 
 
@@ -288,7 +291,7 @@ class Job:
         st = (C.c_double * 8)()
         _check(_lib.bnpp_job_stats(self._h, st, 8), "bnpp_job_stats")
         (self.entries, self.arena_bytes, self.levels, self.buckets, self.width, self.max_table,
-         self.alg_bytes) = st[0], st[1], int(st[2]), int(st[3]), int(st[4]), st[5], st[6]
+         self.alg_bytes, self.batches) = st[0], st[1], int(st[2]), int(st[3]), int(st[4]), st[5], st[6], int(st[7])
 
     def launch(self, stream: Optional[int] = None) -> None:
         _check(_lib.bnpp_job_launch(self._h, _P(stream) if stream else None), "bnpp_job_launch")

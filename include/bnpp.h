@@ -153,10 +153,11 @@ int bnpp_variable_elimination(bnpp_ctx *ctx, const bnpp_model *m, int n_vars, co
                               int dtype, int cap_vars, int *out_ndims, int *out_vars, int64_t cap_values,
                               int64_t *out_size, double *out_values, int64_t *exp2);
 
-/* Host-only planning statistics (no device needed): kind 0 partition, 1 marginals
- * of all variables.  stats as bnpp_job_stats. */
+/* Host-only planning statistics (no device needed): kind 0 partition (explicit
+ * order if `order` is non-NULL), 1 marginals of all variables.  stats as
+ * bnpp_job_stats. */
 int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
-                    int dtype, double *stats, int n_stats);
+                    const int *order, int n_order, int dtype, double *stats, int n_stats);
 
 /* ------------------------------------------- prepared jobs (benchmark) */
 /* A planned, device-resident inference that can be launched repeatedly. */
@@ -166,7 +167,8 @@ int bnpp_job_create(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, cons
                     const int *ev_vals, int heuristic, const int *order, int n_order, int n_targets,
                     const int *targets, int dtype, bnpp_job **out);
 /* stats: [0] factor-entries per launch, [1] arena bytes, [2] levels, [3] buckets,
- *        [4] max induced width, [5] largest message entries, [6] algorithmic bytes */
+ *        [4] max induced width, [5] largest message entries, [6] algorithmic bytes,
+ *        [7] target batches */
 int bnpp_job_stats(const bnpp_job *job, double *stats, int n_stats);
 int bnpp_job_launch(bnpp_job *job, void *stream);
 /* waits on stream; partition: out[0] = log10 Z; marginals: sum(card) values */
