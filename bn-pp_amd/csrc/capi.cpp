@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -172,14 +173,18 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
         }
         plans.push_back(plan_ve(d.cards, views, ord, true));
     } else {
-        for (int t : targets) {
+        // one independent VE per target (model.cpp:326-334), planned in parallel
+        plans.resize(targets.size());
+        std::vector<int> widths(targets.size(), 0);
+        parallel_for((int64_t)targets.size(), [&](int64_t i) {
+            const int t = targets[i];
             std::vector<int> vars, ord;
             for (int v = 0; v < nv; ++v)                 // model.cpp:327-332 (evidence vars are no-ops)
                 if (v != t && ev[v] < 0) vars.push_back(v);
-            int w = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
-            max_width = std::max(max_width, w);
-            plans.push_back(plan_ve(d.cards, views, ord, true));
-        }
+            widths[i] = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
+            plans[i] = plan_ve(d.cards, views, ord, true);
+        });
+        for (int w : widths) max_width = std::max(max_width, w);
     }
     return BNPP_OK;
 }
@@ -191,8 +196,11 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
                    std::vector<Schedule> &out, double *stats) {
     std::vector<VEPlan> plans;
     int width = 0;
+    const bool timing = std::getenv("BNPP_TIMING") != nullptr;
+    double t0 = now_ms();
     int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width);
     if (rc) return rc;
+    if (timing) std::fprintf(stderr, "[bnpp] plans %.1f ms\n", now_ms() - t0);
     const int eb = dtype == BNPP_F32 ? 4 : 8;
     std::vector<int64_t> src_sizes;
     for (auto &v : d.values) src_sizes.push_back((int64_t)v.size());
@@ -221,6 +229,7 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
         buckets += (double)s.descs.size();
         out.push_back(std::move(s));
     }
+    if (timing) std::fprintf(stderr, "[bnpp] schedules %.1f ms total\n", now_ms() - t0);
     stats[0] = entries;
     stats[1] = arena;
     stats[2] = levels;

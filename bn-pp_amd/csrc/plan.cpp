@@ -2,12 +2,35 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
 
 namespace bnpp {
+
+void parallel_for(int64_t n, const std::function<void(int64_t)> &body, int threads) {
+    if (threads <= 0) {
+        threads = (int)std::thread::hardware_concurrency();
+        if (const char *e = std::getenv("BNPP_HOST_THREADS")) threads = std::atoi(e);
+        threads = std::max(1, std::min(threads, 16));
+    }
+    if (n <= 1 || threads == 1) {
+        for (int64_t i = 0; i < n; ++i) body(i);
+        return;
+    }
+    std::atomic<int64_t> next(0);
+    auto worker = [&]() {
+        for (int64_t i = next++; i < n; i = next++) body(i);
+    };
+    std::vector<std::thread> pool;
+    int nt = (int)std::min<int64_t>(threads, n);
+    for (int t = 1; t < nt; ++t) pool.emplace_back(worker);
+    worker();
+    for (auto &t : pool) t.join();
+}
 
 std::vector<int64_t> natural_strides(const std::vector<int> &vars, const std::vector<int> &cards) {
     std::vector<int64_t> s(vars.size());
@@ -491,52 +514,74 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     }
     s.arena_bytes = arena.top;
 
-    // descriptors, level by level
-    std::vector<std::vector<std::pair<size_t, const BucketSpec *>>> by_level(n_levels + 1);
+    // descriptors: built in parallel (one per bucket, private dims-pool rows),
+    // then grouped per level by kernel variant and concatenated
+    struct Item {
+        int level;
+        size_t plan;
+        const BucketSpec *b;
+        BucketDesc d;
+        std::vector<int64_t> pool;
+        int key;
+        bool ok;
+        std::string msg;
+    };
+    std::vector<Item> items;
     for (size_t pi = 0; pi < plans.size(); ++pi)
-        for (const BucketSpec &b : plans[pi]->buckets) by_level[b.level].push_back({pi, &b});
-    for (int L = 1; L <= n_levels; ++L) {
-        std::vector<std::pair<int, BucketDesc>> lv;
-        for (auto &pb : by_level[L]) {
-            BucketSpec b = *pb.second;
-            for (View &v : b.in) v.table = remap(pb.first, v.table);
-            b.out_table = remap(pb.first, b.out_table);
-            BucketDesc d;
-            if (!build_desc(b, cards, max_vec, d, s.pool, msg)) return false;
-            lv.push_back({d.big >= 0 ? stream_key(d.bcls, d.v1, d.v2) : variant_key(d.n_in, d.v1, d.v2), d});
+        for (const BucketSpec &b : plans[pi]->buckets) items.push_back(Item{b.level, pi, &b, BucketDesc{}, {}, 0, true, {}});
+    parallel_for((int64_t)items.size(), [&](int64_t idx) {
+        Item &it = items[idx];
+        BucketSpec b = *it.b;
+        for (View &v : b.in) v.table = remap(it.plan, v.table);
+        b.out_table = remap(it.plan, b.out_table);
+        it.ok = build_desc(b, cards, max_vec, it.d, it.pool, &it.msg);
+        it.key = it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2) : variant_key(it.d.n_in, it.d.v1, it.d.v2);
+    });
+    for (const Item &it : items)
+        if (!it.ok) {
+            if (msg) *msg = it.msg;
+            return false;
         }
-        std::stable_sort(lv.begin(), lv.end(), [](const std::pair<int, BucketDesc> &a,
-                                                  const std::pair<int, BucketDesc> &b) { return a.first < b.first; });
-        if (std::getenv("BNPP_DUMP_PLAN")) {
-            for (auto &e : lv) {
-                const BucketDesc &d = e.second;
-                std::fprintf(stderr, "L%d n_in=%d k=%d tile=%dx%d big=%d bcls=%d tiles=%lld dims:", L, d.n_in, d.k, d.v1,
-                             d.v2, d.big, d.big >= 0 ? d.bcls : 0, (long long)d.n_tiles);
+    std::vector<int> ord(items.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+        return items[a].level != items[b].level ? items[a].level < items[b].level : items[a].key < items[b].key;
+    });
+    size_t pool_total = 0;
+    for (const Item &it : items) pool_total += it.pool.size();
+    s.pool.reserve(pool_total);
+    s.descs.reserve(items.size());
+    const bool dump = std::getenv("BNPP_DUMP_PLAN") != nullptr;
+    for (size_t i = 0; i < ord.size();) {
+        const Item &first = items[ord[i]];
+        Schedule::Group g{first.level, first.key, (int)s.descs.size(), 0, 0, 0};
+        int64_t vb = 0;
+        for (; i < ord.size() && items[ord[i]].level == g.level && items[ord[i]].key == g.variant; ++i) {
+            const Item &it = items[ord[i]];
+            BucketDesc d = it.d;
+            d.dim_off = (int64_t)s.pool.size();
+            s.pool.insert(s.pool.end(), it.pool.begin(), it.pool.end());
+            d.vblk_begin = vb;
+            vb += (d.n_tiles + kBlock - 1) / kBlock;
+            g.small_elems = std::max(g.small_elems, d.big >= 0 ? d.small_elems : 0);
+            if (dump) {
+                std::fprintf(stderr, "L%d n_in=%d k=%d tile=%dx%d big=%d bcls=%d tiles=%lld dims:", g.level, d.n_in, d.k,
+                             d.v1, d.v2, d.big, d.big >= 0 ? d.bcls : 0, (long long)d.n_tiles);
                 for (int j = 0; j < d.n_dims; ++j) {
-                    const int64_t *row = s.pool.data() + d.dim_off + (int64_t)j * (2 + d.n_in);
+                    const int64_t *row = it.pool.data() + (int64_t)j * (2 + d.n_in);
                     std::fprintf(stderr, " [%u:", (unsigned)((uint64_t)row[0] & 0xffffffffu));
-                    for (int i = 0; i < d.n_in; ++i) std::fprintf(stderr, "%s%lld", i ? "," : "", (long long)row[2 + i]);
+                    for (int q = 0; q < d.n_in; ++q) std::fprintf(stderr, "%s%lld", q ? "," : "", (long long)row[2 + q]);
                     std::fprintf(stderr, "]");
                 }
                 std::fprintf(stderr, " es:");
-                for (int i = 0; i < d.n_in; ++i) std::fprintf(stderr, "%s%lld", i ? "," : "", (long long)d.elim_stride[i]);
+                for (int q = 0; q < d.n_in; ++q) std::fprintf(stderr, "%s%lld", q ? "," : "", (long long)d.elim_stride[q]);
                 std::fprintf(stderr, "\n");
             }
+            s.descs.push_back(d);
         }
-        for (size_t i = 0; i < lv.size();) {
-            Schedule::Group g{L, lv[i].first, (int)s.descs.size(), 0, 0, 0};
-            int64_t vb = 0;
-            for (; i < lv.size() && lv[i].first == g.variant; ++i) {
-                BucketDesc d = lv[i].second;
-                g.small_elems = std::max(g.small_elems, d.big >= 0 ? d.small_elems : 0);
-                d.vblk_begin = vb;
-                vb += (d.n_tiles + kBlock - 1) / kBlock;
-                s.descs.push_back(d);
-            }
-            g.end = (int)s.descs.size();
-            g.vblocks = vb;
-            s.groups.push_back(g);
-        }
+        g.end = (int)s.descs.size();
+        g.vblocks = vb;
+        s.groups.push_back(g);
     }
     s.n_levels = n_levels;
     return true;

@@ -1,12 +1,17 @@
 // Host-side planning for the fused bucket kernels (no HIP calls; unit-testable on CPU).
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
 #include "bnpp_device.h"
 
 namespace bnpp {
+
+// Run body(i) for i in [0, n) on up to `threads` host threads (0: hardware
+// concurrency, capped at 16 — the per-GPU CPU share of the target machines).
+void parallel_for(int64_t n, const std::function<void(int64_t)> &body, int threads = 0);
 
 // A table as one bucket input sees it: table id, evidence base offset, and the
 // (variable, stride) pairs that remain after conditioning (domain.cpp:74-90).
