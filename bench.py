@@ -48,6 +48,47 @@ def cpu_baseline(k: int, w_cpu: int, reps: int):
             "sample": sample + " (oracle restatement)", "seconds": sec}
 
 
+def mar_wallclock(ctx, rank, world, dist, dev, rows=12, cols=12):
+    """Second half of the metric: MAR wall-clock (BASELINE config 3 restated to
+    the largest reference-runnable square grid).  All marginals of
+    an R x C Ising grid via VE with min-fill (BN::marginals, model.cpp:303-346),
+    fp64; targets dealt round-robin over ranks and assembled with one
+    all-reduce.  Timed like the reference's uptime (ordering + planning + device
+    run + normalize), max over ranks."""
+    import torch
+    import bnpp
+    from bnpp import synth, dist as bdist
+
+    m = bnpp.Model.from_dict(synth.ising_grid(rows, cols, seed=0))
+
+    def compute(targets):
+        marg, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64, targets=targets)
+        return marg
+
+    compute([0])                                        # warm the code paths
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    marg = bdist.sharded_marginals(m.n_vars, m.cards, rank, world, compute, dist)
+    ms = (time.perf_counter() - t0) * 1e3
+    if dist is not None:
+        tt = torch.tensor([ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ms = tt.item()
+    ref_ms = None
+    ref_file = os.path.join(REPO, "profiles", "r01_ve_bench.jsonl")
+    if os.path.exists(ref_file):
+        for line in open(ref_file):
+            r = json.loads(line)
+            if r.get("instance") == "ising%dx%d" % (rows, cols) and r.get("task") == "MAR" and r.get("ref_ms"):
+                ref_ms = r["ref_ms"]
+    return {"instance": "ising%dx%d all marginals, min-fill, fp64 (config 3 restated)" % (rows, cols),
+            "wall_ms": ms, "n_gpus": world, "p_var0": marg[0],
+            "reference_cpu_ms": ref_ms,
+            "reference_cpu_source": "profiles/r01_ve_bench.jsonl (oracle/_ref ref_harness mar, 1 core of the GPU box)",
+            "speedup_vs_reference": (ref_ms / ms) if ref_ms else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,6 +100,7 @@ def main():
     ap.add_argument("--cpu-w", type=int, default=10, help="bucket width of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-mar", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -141,6 +183,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(k, args.cpu_w, args.cpu_reps)
 
+    mar = None if args.no_mar else mar_wallclock(ctx, rank, world, dist if world > 1 else None, dev)
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -162,6 +206,7 @@ def main():
                          "frac": achieved / HBM_PEAK, "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
                          "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
+            "mar": mar,
             "checksum_ok": ok,
         }
         print(json.dumps(line), flush=True)
