@@ -60,6 +60,15 @@ struct BucketDesc {
     int32_t in_span[kMaxIn];        // elements of each small input's reachable range
 };
 
+// arguments of one level launch (a group of buckets of one kernel variant)
+struct LevelArgs {
+    const BucketDesc *descs;
+    int n_desc;
+    const int64_t *pool;
+    TableMeta *meta;
+    int64_t vblocks;
+};
+
 // loads of the big input of a stream bucket, relative to one thread's tile
 enum BigClass : int32_t { kBigRow = 1, kBigCol = 2, kBigFull = 3, kBigDirect = 4 };
 constexpr int kStreamSmallMax = 4096;      // entries: inputs at most this big go to LDS

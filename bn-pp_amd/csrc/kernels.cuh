@@ -19,6 +19,7 @@
 //     per-workgroup max that is published with one atomicMax per bucket.
 // Inputs whose stride on the fastest output dim is 1 are read with vec-wide
 // loads, stride-0 inputs are broadcast, anything else is gathered.
+#pragma once
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -581,8 +582,11 @@ __device__ __forceinline__ void load_stream_state(StreamState &st, const BucketD
 
 constexpr int kRedBytes = 64;       // block max reduction scratch at the head of dynamic LDS
 
+#ifndef BNPP_STREAM_MINWAVES
+#define BNPP_STREAM_MINWAVES 1
+#endif
 template <typename T, int V1, int V2, int BC>
-__global__ __launch_bounds__(kBlock) void stream_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
+__global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                               const int64_t *__restrict__ pool,
                                                               TableMeta *__restrict__ meta, int64_t total_vblocks) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
@@ -640,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void stream_level_kernel(const BucketDesc *
 }
 
 template <typename T, int V1, int V2, int BC>
-__global__ __launch_bounds__(kBlock) void stream_single_kernel(const SingleArgs args) {
+__global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_single_kernel(const SingleArgs args) {
 #if defined(__HIP_DEVICE_COMPILE__)
     (void)args;
     const SingleArgs &a = *(const __attribute__((address_space(4))) SingleArgs *)__builtin_amdgcn_kernarg_segment_ptr();
@@ -670,13 +674,6 @@ __global__ __launch_bounds__(kBlock) void stream_single_kernel(const SingleArgs 
 }
 
 // ---------------------------------------------------------------- launchers
-struct LevelArgs {
-    const BucketDesc *descs;
-    int n_desc;
-    const int64_t *pool;
-    TableMeta *meta;
-    int64_t vblocks;
-};
 
 template <typename T, int NIN, int V1, int V2>
 static hipError_t go_level(const LevelArgs &a, int max_grid, hipStream_t stream) {
@@ -723,26 +720,6 @@ static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_
 #define BNPP_CASE_SSINGLE(T, V1, V2, BC) \
     case 4096 + BC * 64 + V1 * 8 + V2: return go_stream_single<T, V1, V2, BC>(a, max_grid, stream);
 
-static hipError_t dispatch_stream_level(bool f32, int key, const LevelArgs &a, int small_elems, int max_grid,
-                                        hipStream_t stream) {
-    if (f32) {
-        switch (key) { BNPP_STREAM_F32(BNPP_CASE_SLEVEL, float) default: break; }
-    } else {
-        switch (key) { BNPP_STREAM_F64(BNPP_CASE_SLEVEL, double) default: break; }
-    }
-    return hipErrorInvalidValue;
-}
-
-static hipError_t dispatch_stream_single(bool f32, int key, const SingleArgs &a, int max_grid, hipStream_t stream) {
-    if (f32) {
-        switch (key) { BNPP_STREAM_F32(BNPP_CASE_SSINGLE, float) default: break; }
-    } else {
-        switch (key) { BNPP_STREAM_F64(BNPP_CASE_SSINGLE, double) default: break; }
-    }
-    return hipErrorInvalidValue;
-}
-
-// every (nin class, v1, v2) the planner can produce for T
 #define BNPP_TILES_F32(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
     X(T, NIN, 4, 2) X(T, NIN, 4, 4) X(T, NIN, 2, 8)
 #define BNPP_TILES_F64(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
@@ -754,36 +731,5 @@ static hipError_t dispatch_stream_single(bool f32, int key, const SingleArgs &a,
 #define BNPP_CASE_SINGLE(T, NIN, V1, V2) \
     case NIN * 64 + V1 * 8 + V2: return go_single<T, NIN, V1, V2>(a, max_grid, stream);
 
-static hipError_t dispatch_level(bool f32, int key, const LevelArgs &a, int max_grid, hipStream_t stream) {
-    if (f32) {
-        switch (key) { BNPP_ALL(BNPP_CASE_LEVEL, BNPP_TILES_F32, float) default: break; }
-    } else {
-        switch (key) { BNPP_ALL(BNPP_CASE_LEVEL, BNPP_TILES_F64, double) default: break; }
-    }
-    return hipErrorInvalidValue;
-}
-
-static hipError_t dispatch_single(bool f32, int key, const SingleArgs &a, int max_grid, hipStream_t stream) {
-    if (f32) {
-        switch (key) { BNPP_ALL(BNPP_CASE_SINGLE, BNPP_TILES_F32, float) default: break; }
-    } else {
-        switch (key) { BNPP_ALL(BNPP_CASE_SINGLE, BNPP_TILES_F64, double) default: break; }
-    }
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream) {
-    if (a.d.n_tiles <= 0) return hipSuccess;
-    if (a.d.big >= 0) return dispatch_stream_single(is_f32 != 0, stream_key(a.d.bcls, a.d.v1, a.d.v2), a, max_grid, stream);
-    return dispatch_single(is_f32 != 0, variant_key(a.d.n_in, a.d.v1, a.d.v2), a, max_grid, stream);
-}
-
-hipError_t launch_level(int is_f32, int variant, const BucketDesc *descs, int n_desc, const int64_t *pool,
-                        TableMeta *meta, int64_t total_vblocks, int small_elems, int max_grid, hipStream_t stream) {
-    if (n_desc <= 0 || total_vblocks <= 0) return hipSuccess;
-    LevelArgs a{descs, n_desc, pool, meta, total_vblocks};
-    if (variant >= 4096) return dispatch_stream_level(is_f32 != 0, variant, a, small_elems, max_grid, stream);
-    return dispatch_level(is_f32 != 0, variant, a, max_grid, stream);
-}
 
 }  // namespace bnpp

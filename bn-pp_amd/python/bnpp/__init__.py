@@ -12,6 +12,8 @@ from typing import Dict, Iterable, List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libbnpp.so"))
+if os.environ.get("BNPP_LIB"):          # A/B of alternative builds (experiments only)
+    LIB_PATH = os.environ["BNPP_LIB"]
 
 if not os.path.exists(LIB_PATH):
     raise ImportError("libbnpp.so not built (%s); run `make -C bn-pp_amd` or __graft_entry__.build()" % LIB_PATH)
