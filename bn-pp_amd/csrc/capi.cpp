@@ -172,6 +172,27 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
         plans.push_back(plan_ve(d.cards, views, ord, true));
+    } else if (kind == 3) {
+        // all marginals from one two-pass bucket tree over the PR ordering
+        std::vector<int> vars, ord;
+        if (order) {
+            std::vector<char> seen(nv, 0);
+            for (int i = 0; i < n_order; ++i) {
+                int v = order[i];
+                if (v < 0 || v >= nv || seen[v]) return set_err(BNPP_ERR_INVALID, "bad explicit order");
+                seen[v] = 1;
+                if (ev[v] < 0) vars.push_back(v);
+            }
+            for (int v = 0; v < nv; ++v)
+                if (!seen[v] && ev[v] < 0) return set_err(BNPP_ERR_INVALID, "explicit order must cover every non-evidence variable");
+            ord = vars;
+            max_width = order_width(nv, scopes, ord);
+        } else {
+            for (int v = 0; v < nv; ++v)
+                if (ev[v] < 0) vars.push_back(v);
+            max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
+        }
+        plans.push_back(plan_bucket_tree(d.cards, views, ord, targets));
     } else {
         // one independent VE per target (model.cpp:326-334), planned in parallel
         plans.resize(targets.size());
@@ -208,6 +229,12 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     int64_t acc = 0;
     for (auto &p : plans) {
         int64_t need = plan_peak_bytes(p, eb) + (int64_t)p.buckets.size() * 512;
+        if (kind == 3 && need > budget) {
+            char m[256];
+            std::snprintf(m, sizeof m, "bucket-tree marginals need %.2f GB of messages, budget %.2f GB "
+                          "(per-target marginals or a narrower order)", need / 1e9, budget / 1e9);
+            return set_err(BNPP_ERR_OOM, m);
+        }
         if (!batches.back().empty() && acc + need > budget) {
             batches.emplace_back();
             acc = 0;
@@ -265,7 +292,7 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     job->cards = d.cards;
     std::string msg;
     if (!evidence_array(d, n_ev, ev_vars, ev_vals, job->ev_val, msg)) return set_err(BNPP_ERR_INVALID, msg);
-    if (kind == 1) {
+    if (kind == 1 || kind == 3) {
         if (targets) {
             for (int i = 0; i < n_targets; ++i) {
                 if (targets[i] < 0 || targets[i] >= (int)d.cards.size()) return set_err(BNPP_ERR_INVALID, "bad target");
@@ -371,7 +398,9 @@ int bnpp_ctx_create(int device, bnpp_ctx **out) {
     if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return set_err(BNPP_ERR_HIP, hipGetErrorString(e));
     std::unique_ptr<bnpp_ctx> ctx(new bnpp_ctx);
     ctx->c.device = device;
-    ctx->c.max_grid = prop.multiProcessorCount * 8;
+    int per_cu = 8;
+    if (const char *g = std::getenv("BNPP_GRID_PER_CU")) per_cu = std::max(1, std::min(64, std::atoi(g)));
+    ctx->c.max_grid = prop.multiProcessorCount * per_cu;
     if ((e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking)) != hipSuccess)
         return set_err(BNPP_ERR_HIP, hipGetErrorString(e));
     *out = ctx.release();
@@ -636,7 +665,8 @@ int bnpp_job_create(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, cons
     BNPP_GUARD_BEGIN
     if (!out) return set_err(BNPP_ERR_INVALID, "null output");
     *out = nullptr;
-    if (kind != 0 && kind != 1) return set_err(BNPP_ERR_INVALID, "kind must be 0 (partition) or 1 (marginals)");
+    if (kind != 0 && kind != 1 && kind != 3)
+        return set_err(BNPP_ERR_INVALID, "kind must be 0 (partition), 1 (marginals) or 3 (bucket-tree marginals)");
     std::unique_ptr<bnpp_job> job;
     int rc = create_job(ctx, m, kind, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job);
     if (rc) {
@@ -680,11 +710,11 @@ int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars,
                     const int *order, int n_order, int dtype, double *stats, int n_stats) {
     BNPP_GUARD_BEGIN
     if (!m || !stats) return set_err(BNPP_ERR_INVALID, "null argument");
-    if (kind != 0 && kind != 1) return set_err(BNPP_ERR_INVALID, "kind must be 0 or 1");
+    if (kind != 0 && kind != 1 && kind != 3) return set_err(BNPP_ERR_INVALID, "kind must be 0, 1 or 3");
     std::vector<int> ev, targets;
     std::string msg;
     if (!evidence_array(m->d, n_ev, ev_vars, ev_vals, ev, msg)) return set_err(BNPP_ERR_INVALID, msg);
-    if (kind == 1)
+    if (kind == 1 || kind == 3)
         for (int v = 0; v < (int)m->d.cards.size(); ++v) targets.push_back(v);
     std::vector<Schedule> batches;
     double st[8] = {0};
@@ -748,6 +778,23 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     double t0 = now_ms();
     std::unique_ptr<bnpp_job> job;
     int rc = create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, job);
+    if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
+    if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
+    if (job) destroy_job(job.release());
+    if (rc) return rc;
+    if (uptime_ms) *uptime_ms = now_ms() - t0;
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_marginals_tree(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                        int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
+                        double *out, double *uptime_ms) {
+    BNPP_GUARD_BEGIN
+    if (!out) return set_err(BNPP_ERR_INVALID, "null output");
+    double t0 = now_ms();
+    std::unique_ptr<bnpp_job> job;
+    int rc = create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job);
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
     if (job) destroy_job(job.release());

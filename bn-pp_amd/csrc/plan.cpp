@@ -249,8 +249,19 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         if (n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 && !(off && *off == '1')) {
             int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
             int64_t s1 = merged.size() < 2 ? 0 : merged[1].s[big];
+            // optional narrow tile: when the big input is constant along the
+            // fastest output dim and v1 entries already fill a 16-B store, drop
+            // v2 (one scalar big load per summed value, stores coalesced as is)
+            const char *nw = std::getenv("BNPP_NARROW");
+            if (nw && *nw == '1' && v2 > 1 && s0 == 0 && v1 * eb >= 16) {
+                v2 = 1;
+                d.v2 = 1;
+                d.n_tiles = out_size / v1;
+                divisor(merged.size() < 2 ? 1 : merged[1].card, d.tdiv1);
+            }
             int bc;
-            if (v1 > 1 && s0 == 1 && (v2 == 1 || s1 == 0)) bc = kBigRow;
+            if (s0 == 0 && (v2 == 1 || s1 == 0)) bc = kBigOne;
+            else if (v1 > 1 && s0 == 1 && (v2 == 1 || s1 == 0)) bc = kBigRow;
             else if (v2 > 1 && s0 == 0 && s1 == 1) bc = kBigCol;
             else if (v1 > 1 && v2 > 1 && s0 == 1 && s1 == v1) bc = kBigFull;
             else bc = kBigDirect;
@@ -278,26 +289,36 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
 }
 
 // ---------------------------------------------------------------- VE plan
-VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, const std::vector<int> &order,
-               bool canonical) {
-    VEPlan p;
-    p.n_src = (int)sources.size();
-    const int nv = (int)cards.size();
-    std::vector<int> rank(nv, -1);
-    for (int i = (int)order.size() - 1; i >= 0; --i) rank[order[i]] = i;
+namespace {
+// Emits buckets and message tables into a VEPlan (shared by plan_ve and
+// plan_bucket_tree).  Levels: a bucket runs one level after its latest input.
+struct PlanBuilder {
+    const std::vector<int> &cards;
+    VEPlan &p;
+    bool canonical;
+    std::vector<int> rank;
+    std::vector<int> level;                 // per table
 
+    PlanBuilder(const std::vector<int> &c, VEPlan &plan, const std::vector<View> &sources,
+                const std::vector<int> &order, bool canon_layout)
+        : cards(c), p(plan), canonical(canon_layout) {
+        p.n_src = (int)sources.size();
+        rank.assign(cards.size(), -1);
+        for (int i = (int)order.size() - 1; i >= 0; --i) rank[order[i]] = i;
+        level.assign(p.n_src, 0);
+    }
     // layout key: earlier-eliminated variables are slower; kept variables last
-    auto canon = [&](std::vector<int> s) {
+    std::vector<int> canon(std::vector<int> s) const {
         if (!canonical) return s;
+        const int64_t nv = (int64_t)cards.size();
         std::stable_sort(s.begin(), s.end(), [&](int a, int b) {
-            int64_t ka = rank[a] >= 0 ? rank[a] : (int64_t)nv + a;
-            int64_t kb = rank[b] >= 0 ? rank[b] : (int64_t)nv + b;
+            int64_t ka = rank[a] >= 0 ? rank[a] : nv + a;
+            int64_t kb = rank[b] >= 0 ? rank[b] : nv + b;
             return ka < kb;
         });
         return s;
-    };
-    std::vector<int> level(p.n_src, 0);     // per table
-    auto new_msg = [&](const std::vector<int> &vars) {
+    }
+    int new_msg(const std::vector<int> &vars) {
         MsgTable t;
         t.vars = vars;
         t.size = table_size(vars, cards);
@@ -305,42 +326,19 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
         p.msgs.push_back(t);
         level.push_back(0);
         return p.n_src + (int)p.msgs.size() - 1;
-    };
-    auto table_view = [&](int id) { return natural_view(id, p.msgs[id - p.n_src].vars, cards); };
-    auto entries_of = [&](const std::vector<View> &in) {
+    }
+    View view(int id) const { return natural_view(id, p.msgs[id - p.n_src].vars, cards); }
+    double entries_of(const std::vector<View> &in) const {
         double e = 1;
         for (int v : chain_scope(in)) e *= cards[v];
         return e;
-    };
-    auto moved_of = [&](const std::vector<View> &in, int out_table) {
+    }
+    double moved_of(const std::vector<View> &in, int out_table) const {
         double e = (double)p.msgs[out_table - p.n_src].size;
         for (const View &v : in) e += (double)table_size(v.vars, cards);
         return e;
-    };
-    // emit a bucket over `in` (any length) summing out `x` (-1: none) into a table laid out as `layout(vars)`
-    auto emit = [&](std::vector<View> in, int x, bool final_result) -> int {
-        while ((int)in.size() > kMaxIn) {
-            std::vector<View> head(in.begin(), in.begin() + kMaxIn);
-            std::vector<int> hv = canon(chain_scope(head));
-            BucketSpec b;
-            b.in = head;
-            b.out_vars = hv;
-            b.out_table = new_msg(hv);
-            int lv = 0;
-            for (const View &v : head) lv = std::max(lv, level[v.table]);
-            b.level = lv + 1;
-            level[b.out_table] = b.level;
-            p.entries += entries_of(head);
-            p.elems_moved += moved_of(head, b.out_table);
-            std::vector<View> rest;
-            rest.push_back(table_view(b.out_table));
-            rest.insert(rest.end(), in.begin() + kMaxIn, in.end());
-            p.buckets.push_back(b);
-            in.swap(rest);
-        }
-        std::vector<int> u = chain_scope(in);
-        std::vector<int> ov = x >= 0 ? remove_var(u, x) : u;
-        if (!final_result) ov = canon(ov);
+    }
+    int push_bucket(const std::vector<View> &in, int x, const std::vector<int> &ov) {
         BucketSpec b;
         b.in = in;
         b.elim_var = x;
@@ -352,43 +350,152 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
         level[b.out_table] = b.level;
         p.entries += entries_of(in);
         p.elems_moved += moved_of(in, b.out_table);
-        p.width = std::max(p.width, (int)ov.size());
         p.buckets.push_back(b);
         return b.out_table;
-    };
-
-    const int nord = (int)order.size();
-    std::vector<std::vector<View>> buckets(nord);
-    std::vector<View> result;
-    auto first_bucket = [&](const std::vector<int> &vars, int from) {
+    }
+    // a bucket over `in` (any length) summing out `x` (-1: none); inputs past
+    // kMaxIn are folded into materialised products left to right, like the
+    // reference's chain
+    int emit(std::vector<View> in, int x, bool final_result) {
+        while ((int)in.size() > kMaxIn) {
+            std::vector<View> head(in.begin(), in.begin() + kMaxIn);
+            int t = push_bucket(head, -1, canon(chain_scope(head)));
+            std::vector<View> rest;
+            rest.push_back(view(t));
+            rest.insert(rest.end(), in.begin() + kMaxIn, in.end());
+            in.swap(rest);
+        }
+        std::vector<int> u = chain_scope(in);
+        std::vector<int> ov = x >= 0 ? remove_var(u, x) : u;
+        if (!final_result) ov = canon(ov);
+        int t = push_bucket(in, x, ov);
+        p.width = std::max(p.width, (int)ov.size());
+        return t;
+    }
+    // first bucket (by elimination rank >= from) whose variable is in `vars`
+    int first_bucket(const std::vector<int> &vars, int from) const {
         int best = -1;
         for (int v : vars) {
-            int r = v < nv ? rank[v] : -1;
+            int r = v < (int)cards.size() ? rank[v] : -1;
             if (r >= from && (best < 0 || r < best)) best = r;
         }
         return best;
-    };
+    }
+    void finish() {
+        std::stable_sort(p.buckets.begin(), p.buckets.end(),
+                         [](const BucketSpec &a, const BucketSpec &b) { return a.level < b.level; });
+        p.n_levels = p.buckets.empty() ? 0 : p.buckets.back().level;
+    }
+};
+}  // namespace
+
+VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, const std::vector<int> &order,
+               bool canonical) {
+    VEPlan p;
+    PlanBuilder B(cards, p, sources, order, canonical);
+    const int nord = (int)order.size();
+    std::vector<std::vector<View>> buckets(nord);
+    std::vector<View> result;
     for (const View &s : sources) {                                   // model.cpp:394-406
-        int bi = first_bucket(s.vars, 0);
+        int bi = B.first_bucket(s.vars, 0);
         if (bi >= 0) buckets[bi].push_back(s);
         else result.push_back(s);
     }
     for (int i = 0; i < nord; ++i) {                                  // model.cpp:409-439
         if (buckets[i].empty()) continue;   // Factor(1.0).sum_out(x) == 1: result *= 1 is exact
-        int t = emit(buckets[i], order[i], false);
-        View mv = table_view(t);
-        int bi = first_bucket(mv.vars, i + 1);
+        int t = B.emit(buckets[i], order[i], false);
+        View mv = B.view(t);
+        int bi = B.first_bucket(mv.vars, i + 1);
         if (bi >= 0) buckets[bi].push_back(mv);
         else result.push_back(mv);
     }
     if (!result.empty()) {
-        p.result_table = emit(result, -1, true);
+        p.result_table = B.emit(result, -1, true);
         p.result_vars = p.msgs[p.result_table - p.n_src].vars;
     }
-    // order buckets by level (stable), levels are 1-based
-    std::stable_sort(p.buckets.begin(), p.buckets.end(),
-                     [](const BucketSpec &a, const BucketSpec &b) { return a.level < b.level; });
-    p.n_levels = p.buckets.empty() ? 0 : p.buckets.back().level;
+    B.finish();
+    return p;
+}
+
+VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &sources,
+                        const std::vector<int> &order, const std::vector<int> &targets) {
+    VEPlan p;
+    PlanBuilder B(cards, p, sources, order, true);
+    const int nord = (int)order.size();
+    // forward (collect) pass: exactly the VE buckets of plan_ve, remembering the tree
+    std::vector<std::vector<View>> src_in(nord);
+    std::vector<std::vector<int>> children(nord);
+    std::vector<int> lam(nord, -1);
+    for (const View &s : sources) {
+        int bi = B.first_bucket(s.vars, 0);
+        if (bi >= 0) src_in[bi].push_back(s);   // else: a constant, cancels in every marginal
+    }
+    auto lam_view = [&](int c) { return B.view(lam[c]); };
+    for (int i = 0; i < nord; ++i) {
+        std::vector<View> in = src_in[i];
+        for (int c : children[i]) in.push_back(lam_view(c));
+        if (in.empty()) continue;
+        lam[i] = B.emit(in, order[i], false);
+        int par = B.first_bucket(p.msgs[lam[i] - p.n_src].vars, i + 1);
+        if (par >= 0) children[par].push_back(i);
+    }
+    // sum everything in `in` except `keep` (elimination-rank order): one fused
+    // bucket for the first variable, then single-input sums
+    auto reduce = [&](const std::vector<View> &in, const std::vector<int> &keep, bool materialise) -> View {
+        std::vector<int> y;
+        for (int v : chain_scope(in))
+            if (std::find(keep.begin(), keep.end(), v) == keep.end()) y.push_back(v);
+        std::sort(y.begin(), y.end(), [&](int a, int b) { return B.rank[a] < B.rank[b]; });
+        if (y.empty()) {
+            if (in.size() == 1 && !(materialise && (in[0].table < p.n_src || in[0].base != 0))) return in[0];
+            return B.view(B.emit(in, -1, false));
+        }
+        int t = B.emit(in, y[0], false);
+        for (size_t j = 1; j < y.size(); ++j) t = B.emit({B.view(t)}, y[j], false);
+        return B.view(t);
+    };
+    // backward (distribute) pass, parents before children:
+    // pi_i = sum_{scope(p) \ sep_i} F_p * pi_p * prod_{c != i} lam_c
+    std::vector<View> pi(nord);
+    std::vector<char> has_pi(nord, 0);
+    for (int q = nord - 1; q >= 0; --q) {
+        if (lam[q] < 0) continue;
+        for (int i : children[q]) {
+            std::vector<View> in = src_in[q];
+            if (has_pi[q]) in.push_back(pi[q]);
+            for (int c : children[q])
+                if (c != i) in.push_back(lam_view(c));
+            if (in.empty()) continue;                    // constant 1
+            pi[i] = reduce(in, p.msgs[lam[i] - p.n_src].vars, false);
+            has_pi[i] = 1;
+        }
+    }
+    // marginals: the belief of the target's bucket, or of the smallest
+    // separator below it (lam_c * pi_c), summed down to the target
+    for (int t : targets) {
+        int i = t >= 0 && t < (int)cards.size() ? B.rank[t] : -1;
+        if (i < 0 || lam[i] < 0) {                       // evidence / not eliminated / in no factor
+            p.results.push_back(-1);
+            p.results_vars.push_back({});
+            continue;
+        }
+        std::vector<View> best = src_in[i];
+        if (has_pi[i]) best.push_back(pi[i]);
+        for (int c : children[i]) best.push_back(lam_view(c));
+        double best_size = (double)table_size(chain_scope(best), cards);
+        for (int c : children[i]) {
+            double sz = (double)p.msgs[lam[c] - p.n_src].size;
+            if (sz < best_size) {
+                best = {lam_view(c)};
+                if (has_pi[c]) best.push_back(pi[c]);
+                best_size = sz;
+            }
+        }
+        View r = reduce(best, {t}, true);
+        p.results.push_back(r.table);
+        p.results_vars.push_back(r.vars);
+    }
+    B.finish();
     return p;
 }
 
@@ -400,6 +507,8 @@ int64_t plan_peak_bytes(const VEPlan &p, int elem_bytes) {
         for (const View &v : b.in) last[v.table] = std::max(last[v.table], b.level);
     }
     if (p.result_table >= 0) last[p.result_table] = p.n_levels + 1;
+    for (int r : p.results)
+        if (r >= 0) last[r] = p.n_levels + 1;
     std::vector<int64_t> delta(p.n_levels + 3, 0);
     for (int t = p.n_src; t < nt; ++t) {
         int64_t bytes = ((p.msgs[t - p.n_src].size * elem_bytes + 255) / 256) * 256;
@@ -498,9 +607,17 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 last[t] = std::max(last[t], b.level);
             }
         }
-        if (plans[pi]->result_table >= 0) last[remap(pi, plans[pi]->result_table)] = kForever;
-        s.plan_result_table.push_back(plans[pi]->result_table >= 0 ? remap(pi, plans[pi]->result_table) : -1);
-        s.plan_result_vars.push_back(plans[pi]->result_vars);
+        std::vector<int> res = plans[pi]->results;
+        std::vector<std::vector<int>> res_vars = plans[pi]->results_vars;
+        if (res.empty()) {                      // single-result plan (PR / one MAR target / VE)
+            res.push_back(plans[pi]->result_table);
+            res_vars.push_back(plans[pi]->result_vars);
+        }
+        for (size_t r = 0; r < res.size(); ++r) {
+            if (res[r] >= 0) last[remap(pi, res[r])] = kForever;
+            s.plan_result_table.push_back(res[r] >= 0 ? remap(pi, res[r]) : -1);
+            s.plan_result_vars.push_back(res_vars[r]);
+        }
     }
     std::vector<std::vector<int>> born_at(n_levels + 2), dies_at(n_levels + 2);
     for (int t = s.n_src; t < s.n_tables; ++t) {

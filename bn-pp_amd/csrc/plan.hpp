@@ -62,6 +62,10 @@ struct VEPlan {
     int n_levels = 0;
     int result_table = -1;              // -1: result is the constant 1 (no factors)
     std::vector<int> result_vars;
+    // multi-result plans (bucket-tree marginals): one table per target, -1 =
+    // no table (evidence / variable in no factor); replaces result_table
+    std::vector<int> results;
+    std::vector<std::vector<int>> results_vars;
     int64_t max_table = 0;              // largest message entries
     double entries = 0;                 // sum over buckets of prod(card) over the union scope
     double elems_moved = 0;             // sum over buckets of (|inputs| + |output|): algorithmic traffic
@@ -75,6 +79,16 @@ struct VEPlan {
 // the reference's left-to-right chain.
 VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, const std::vector<int> &order,
                bool canonical);
+
+// All marginals of `targets` from one two-pass bucket tree over `order`
+// (Shafer-Shenoy on the VE bucket tree; replaces the N independent VEs of
+// BN::marginals, model.cpp:326-334).  Forward messages are plan_ve's; each
+// bucket then sends every child the product of its factors, its own incoming
+// message and its other children's messages, summed down to the child's
+// separator; each target's marginal (unnormalised) is the smallest belief that
+// contains it summed down to the target.  results[i] -> targets[i].
+VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &sources,
+                        const std::vector<int> &order, const std::vector<int> &targets);
 
 // Flattened, level-ordered launch schedule over one or more plans sharing the
 // same sources.  Tables: [0, n_src) sources, then every plan's messages.

@@ -57,6 +57,7 @@ _SIGS = {
     "bnpp_ordering": (_I, [_P, _I, _IP, _IP, _I, _IP, _I, _IP, _IP]),
     "bnpp_partition": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _DP, _DP, _DP]),
     "bnpp_marginals": (_I, [_P, _P, _I, _IP, _IP, _I, _I, _IP, _I, _DP, _DP]),
+    "bnpp_marginals_tree": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, _DP, _DP]),
     "bnpp_variable_elimination": (_I, [_P, _P, _I, _IP, _I, _I, _I, _IP, _IP, C.c_int64, C.POINTER(C.c_int64), _DP,
                                        C.POINTER(C.c_int64)]),
     "bnpp_plan_stats": (_I, [_P, _I, _I, _IP, _IP, _I, _IP, _I, _I, _DP, _I]),
@@ -259,6 +260,27 @@ def marginals(ctx: Context, model: Model, evidence=None, heuristic: str = "mf", 
     return res, up.value
 
 
+def marginals_tree(ctx: Context, model: Model, evidence=None, heuristic: str = "mf", dtype: int = F64,
+                   targets: Optional[Sequence[int]] = None, order: Optional[Sequence[int]] = None):
+    """All marginals from one two-pass bucket tree (bnpp_marginals_tree) ->
+    ({var: [p_0..p_k-1]}, uptime_ms).  Same output as marginals(), to rounding."""
+    n, ev_v, ev_x = _ev(evidence)
+    tg = list(range(model.n_vars)) if targets is None else list(targets)
+    total = sum(model.cards[t] for t in tg)
+    out = (C.c_double * max(total, 1))()
+    up = C.c_double()
+    oa = _ints(list(order)) if order is not None else None
+    h = ORDER_GIVEN if order is not None else HEURISTICS[heuristic]
+    _check(_lib.bnpp_marginals_tree(ctx.handle, model.handle, n, ev_v, ev_x, h, oa,
+                                    len(order) if order is not None else 0, len(tg), _ints(tg), dtype, out,
+                                    C.byref(up)), "bnpp_marginals_tree")
+    res, o = {}, 0
+    for t in tg:
+        res[t] = list(out[o:o + model.cards[t]])
+        o += model.cards[t]
+    return res, up.value
+
+
 def variable_elimination(ctx: Context, model: Model, variables: Sequence[int], heuristic: str = "given",
                          dtype: int = F64, cap_values: int = 1 << 20):
     """BN::variable_elimination over the model's factors as given ->
@@ -282,7 +304,7 @@ class Job:
                  dtype: int = F64, order: Optional[Sequence[int]] = None, targets: Optional[Sequence[int]] = None):
         n, ev_v, ev_x = _ev(evidence)
         self.model = model
-        self.kind = 0 if kind == "pr" else 1
+        self.kind = {"pr": 0, "mar": 1, "mar_tree": 3}[kind]
         self.targets = list(range(model.n_vars)) if targets is None else list(targets)
         self._h = _P()
         order_arr = _ints(order) if order is not None else None

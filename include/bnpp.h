@@ -144,6 +144,19 @@ int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
 int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
                    int heuristic, int n_targets, const int *targets, int dtype, double *out, double *uptime_ms);
 
+/* All marginals from ONE two-pass bucket tree (Shafer-Shenoy message passing
+ * on the VE bucket tree of the partition's elimination order) instead of one VE
+ * per target (model.cpp:326-334): about three VE passes of device work and one
+ * host ordering, whatever the number of targets.  Same output as
+ * bnpp_marginals (normalised, evidence one-hot); values agree with the
+ * reference to rounding (not bit-exact: the sums are associated differently).
+ * order: explicit elimination order covering every non-evidence variable
+ * (heuristic BNPP_ORDER_GIVEN), or NULL.  BNPP_ERR_OOM when every forward
+ * message cannot stay resident within the memory budget. */
+int bnpp_marginals_tree(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                        int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
+                        double *out, double *uptime_ms);
+
 /* BN::variable_elimination (model.cpp:348-446) over the factors of `m` taken
  * as given (already conditioned by the caller): eliminates `vars` (heuristic
  * order, or exactly this order with BNPP_ORDER_GIVEN) and returns the result
@@ -154,7 +167,8 @@ int bnpp_variable_elimination(bnpp_ctx *ctx, const bnpp_model *m, int n_vars, co
                               int64_t *out_size, double *out_values, int64_t *exp2);
 
 /* Host-only planning statistics (no device needed): kind 0 partition (explicit
- * order if `order` is non-NULL), 1 marginals of all variables.  stats as
+ * order if `order` is non-NULL), 1 marginals of all variables (one VE each),
+ * 3 bucket-tree marginals of all variables.  stats as
  * bnpp_job_stats. */
 int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
                     const int *order, int n_order, int dtype, double *stats, int n_stats);
@@ -162,7 +176,8 @@ int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars,
 /* ------------------------------------------- prepared jobs (benchmark) */
 /* A planned, device-resident inference that can be launched repeatedly. */
 typedef struct bnpp_job bnpp_job;
-/* kind 0: partition (targets ignored)   kind 1: marginals of `targets` */
+/* kind 0: partition (targets ignored)   kind 1: marginals of `targets` (one VE
+ * each)   kind 3: marginals of `targets` from one bucket tree */
 int bnpp_job_create(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars,
                     const int *ev_vals, int heuristic, const int *order, int n_order, int n_targets,
                     const int *targets, int dtype, bnpp_job **out);

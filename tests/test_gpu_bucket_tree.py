@@ -1,0 +1,126 @@
+"""GPU parity of the two-pass bucket-tree marginals (bnpp_marginals_tree).
+
+The reference computes each marginal with its own VE (model.cpp:326-334); the
+bucket tree computes all of them from one forward and one backward pass over
+the partition's bucket tree, so its sums are associated differently: parity is
+to rounding, not bit-exact.  Tolerances: fp64 1e-12 absolute against the
+oracle's marginals and the golden vectors; fp32 1e-5 absolute (north star:
+PR/MAR within 1e-6 relative on Z-scale quantities; marginals are in [0, 1]).
+"""
+import os
+
+import pytest
+
+import bnpp
+import refcpu
+from bnpp import synth
+from conftest import evidence_of, model_path
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    return all(abs(x - y) <= tol for x, y in zip(a, b)) and len(a) == len(b)
+
+
+@pytest.mark.parametrize("dtype", [bnpp.F64, bnpp.F32])
+def test_tree_marginals_vs_golden(ctx, golden_ve, dtype):
+    tol = 1e-12 if dtype == bnpp.F64 else 1e-5
+    for case in golden_ve["mar"]:
+        m = bnpp.Model.load(model_path(case["model"]))
+        ev = evidence_of(case["evidence"])
+        marg, _ = bnpp.marginals_tree(ctx, m, ev, case["heuristic"], dtype)
+        for t, ref in case["marginals"].items():
+            t = int(t)
+            if not ref["scope"]:                          # evidence variable: one-hot
+                assert marg[t][ev[t]] == 1.0 and sum(marg[t]) == 1.0
+                continue
+            assert _close(marg[t], ref["values"], tol), (case["model"], t, marg[t], ref["values"])
+
+
+@pytest.mark.parametrize("name,evid", [("alarm.uai", "alarm.uai.evid"), ("network.uai", "network.uai.evid"),
+                                       ("grid3x3.uai", "grid3x3-MAR.uai.evid"), ("ising6x6.uai", None)])
+def test_tree_matches_oracle_per_target(ctx, name, evid):
+    m = bnpp.Model.load(model_path(name))
+    ev = bnpp.load_evidence(model_path(evid)) if evid else {}
+    rm, _ = refcpu.Model.load(model_path(name)).marginals(ev, "mf")
+    marg, _ = bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F64)
+    for t in range(m.n_vars):
+        if t in ev:
+            assert marg[t] == [1.0 if s == ev[t] else 0.0 for s in range(m.cards[t])]
+        else:
+            assert _close(marg[t], rm[t], 1e-12), (name, t, marg[t], rm[t])
+
+
+@pytest.mark.parametrize("spec", [("potts", 5, 5, 3), ("ising", 9, 7, 2), ("noisy_or", 0, 0, 2)])
+def test_tree_matches_per_target_engine(ctx, tmp_path, spec):
+    """Synthetic models (Potts k=3, a non-square Ising grid, a noisy-OR BN with
+    evidence on the findings): tree == per-target VE on the device."""
+    kind, r, c, _ = spec
+    if kind == "potts":
+        md = synth.potts_grid(r, c, k=3, seed=5)
+        ev = {}
+    elif kind == "ising":
+        md = synth.ising_grid(r, c, seed=6)
+        ev = {0: 1, r * c - 1: 0, 17: 1}
+    else:
+        md = synth.noisy_or_bn(14, 18, 3, seed=7)
+        ev = {v: v % 2 for v in range(14, 14 + 18, 2)}
+    m = bnpp.Model.from_dict(md)
+    want, _ = bnpp.marginals(ctx, m, ev, "mf", bnpp.F64)
+    got, _ = bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F64)
+    for t in range(m.n_vars):
+        assert _close(got[t], want[t], 1e-12), (spec, t, got[t], want[t])
+    got32, _ = bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F32)
+    for t in range(m.n_vars):
+        assert _close(got32[t], want[t], 1e-5), (spec, t, got32[t], want[t])
+
+
+def test_tree_explicit_order_and_target_subset(ctx):
+    """A column-sweep order (a chain-shaped bucket tree) and a subset of targets
+    in caller order."""
+    m = bnpp.Model.from_dict(synth.ising_grid(8, 12, seed=8))
+    col = [r * 12 + c for c in range(12) for r in range(8)]
+    want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    targets = [95, 0, 40, 41, 7]
+    got, _ = bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64, targets=targets, order=col)
+    assert list(got) == targets
+    for t in targets:
+        assert _close(got[t], want[t], 1e-12), (t, got[t], want[t])
+
+
+def test_tree_20x20_consistent_with_conditioned_partitions(ctx):
+    """Beyond the per-target path's reach in a test budget: marginals of a
+    20x20 grid (column-sweep order, width 20) match Z(x_t = s) / Z."""
+    m = bnpp.Model.from_dict(synth.ising_grid(20, 20, seed=9))
+    col = [r * 20 + c for c in range(20) for r in range(20)]
+    marg, _ = bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64, order=col)
+    for t, p in marg.items():
+        assert abs(sum(p) - 1.0) < 1e-12
+    lz = bnpp.partition(ctx, m, {}, "mf", bnpp.F64, order=col)[0]
+    for t in (0, 210, 399):
+        for s in range(2):
+            lzs = bnpp.partition(ctx, m, {t: s}, "mf", bnpp.F64, order=col)[0]
+            assert abs(10 ** (lzs - lz) - marg[t][s]) < 1e-11, (t, s)
+
+
+def test_tree_memory_budget_is_enforced(ctx):
+    m = bnpp.Model.from_dict(synth.ising_grid(10, 10, seed=0))
+    os.environ["BNPP_MEM_BUDGET_GB"] = "1e-7"
+    try:
+        with pytest.raises(bnpp.BnppError) as e:
+            bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64)
+        assert e.value.status == bnpp.ERR_OOM
+    finally:
+        del os.environ["BNPP_MEM_BUDGET_GB"]
+
+
+def test_tree_job_relaunch(ctx):
+    m = bnpp.Model.from_dict(synth.ising_grid(7, 7, seed=1))
+    job = bnpp.Job(ctx, m, "mar_tree", heuristic="mf", dtype=bnpp.F64)
+    job.launch()
+    a = job.results()
+    job.launch()
+    job.launch()
+    assert job.results() == a
+    job.close()

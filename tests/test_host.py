@@ -123,3 +123,30 @@ def test_bad_arguments_are_rejected():
     with pytest.raises(bnpp.BnppError) as e:
         bnpp.plan_stats(m, 7)                # unknown job kind
     assert e.value.status == bnpp.ERR_INVALID
+
+
+def test_plan_stats_bucket_tree():
+    """kind 3 (bucket-tree marginals) plans about three VE passes for ALL
+    targets, far less than one VE per target (kind 1)."""
+    m = bnpp.Model.load(model_path("ising10x10.uai"))
+    pr = bnpp.plan_stats(m, 0, {}, "mf")
+    tree = bnpp.plan_stats(m, 3, {}, "mf")
+    per_target = bnpp.plan_stats(m, 1, {}, "mf")
+    assert tree[4] == pr[4]                            # same ordering, same width
+    assert pr[0] < tree[0] < 6 * pr[0]                 # factor-entries: a few passes
+    assert tree[0] < per_target[0] / 10
+    assert tree[7] == 1                                # one schedule
+    col = [r * 10 + c for c in range(10) for r in range(10)]
+    st = bnpp.plan_stats(m, 3, {}, "mf", order=col)
+    assert st[4] == 10
+    with pytest.raises(bnpp.BnppError) as e:           # explicit order must cover every variable
+        bnpp.plan_stats(m, 3, {}, "mf", order=col[:-1])
+    assert e.value.status == bnpp.ERR_INVALID
+
+
+def test_bucket_tree_rejects_null_context():
+    m = bnpp.Model.load(model_path("grid3x3.uai"))
+    null_ctx = type("NullCtx", (), {"handle": None})()
+    with pytest.raises(bnpp.BnppError) as e:
+        bnpp.marginals_tree(null_ctx, m)
+    assert e.value.status == bnpp.ERR_INVALID

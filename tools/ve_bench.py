@@ -50,7 +50,9 @@ def main():
     ctx = bnpp.Context(0)
     cases = [("ising10x10", 10, 10, "mar"), ("ising12x12", 12, 12, "mar"), ("ising12x32", 12, 32, "pr"),
              ("ising12x32", 12, 32, "mar"), ("ising16x16", 16, 16, "pr"), ("ising16x16", 16, 16, "mar"),
-             ("ising20x20", 20, 20, "pr"), ("ising32x32-col", 32, 32, "pr")]
+             ("ising20x20", 20, 20, "pr"), ("ising32x32-col", 32, 32, "pr"),
+             ("ising12x12", 12, 12, "mar_tree"), ("ising12x32-col", 12, 32, "mar_tree"),
+             ("ising16x16", 16, 16, "mar_tree"), ("ising20x20-col", 20, 20, "mar_tree")]
     tmp = tempfile.mkdtemp()
     for name, r, c, kind in cases:
         if args.only and args.only not in name:
@@ -63,15 +65,18 @@ def main():
         if name.endswith("-col"):          # width-32 column sweep (SURVEY 8(d), config 3 restated)
             order = [rr * c + cc for cc in range(c) for rr in range(r)]
         for dtype in (bnpp.F32, bnpp.F64):
-            if name.endswith("-col") and dtype == bnpp.F64:
+            if name.startswith("ising32x32") and dtype == bnpp.F64:
                 continue
             rec = {"instance": name, "task": kind.upper(), "dtype": "f32" if dtype == bnpp.F32 else "f64"}
             t0 = time.perf_counter()
             if kind == "pr":
                 lz, _, up = bnpp.partition(ctx, m, {}, "mf", dtype, order=order)
                 rec["log10Z"] = lz
-            else:
+            elif kind == "mar":
                 marg, up = bnpp.marginals(ctx, m, {}, "mf", dtype)
+                rec["p0"] = marg[0]
+            else:
+                marg, up = bnpp.marginals_tree(ctx, m, {}, "mf", dtype, order=order)
                 rec["p0"] = marg[0]
             rec["gpu_uptime_ms"] = up
             rec["gpu_call_ms"] = (time.perf_counter() - t0) * 1e3
@@ -89,7 +94,7 @@ def main():
                         "arena_GB": job.arena_bytes / 1e9, "alg_GB": job.alg_bytes / 1e9,
                         "batches": job.batches})
             job.close()
-            if args.ref and dtype == bnpp.F64 and not name.endswith("-col") and not (r * c > 256 and kind == "mar"):
+            if args.ref and dtype == bnpp.F64 and kind != "mar_tree" and not name.endswith("-col") and not (r * c > 256 and kind == "mar"):
                 rec["ref_ms"] = ref_time(kind, path, args.ref_timeout)
             print(json.dumps(rec), flush=True)
 
