@@ -141,7 +141,8 @@ std::vector<View> source_views(const ModelData &d, const std::vector<int> &ev) {
 
 // Build the VE plans for a job: kind 0 = partition, kind 1 = marginals of targets.
 int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
-                int n_order, const std::vector<int> &targets, std::vector<VEPlan> &plans, int &max_width) {
+                int n_order, const std::vector<int> &targets, std::vector<VEPlan> &plans, int &max_width,
+                int64_t budget, int eb) {
     const int nv = (int)d.cards.size();
     auto scopes = conditioned_scopes(d, ev);
     auto views = source_views(d, ev);
@@ -193,6 +194,37 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
         plans.push_back(plan_bucket_tree(d.cards, views, ord, targets));
+        auto need = [&](const VEPlan &p) { return plan_peak_bytes(p, eb) + (int64_t)p.buckets.size() * 512; };
+        const char *force = std::getenv("BNPP_TREE_SLOTS");     // testing / tuning: chain mode, fixed slots
+        if (force && std::atoi(force) > 0) {
+            std::string msg;
+            VEPlan cp;
+            if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), cp, &msg))
+                return set_err(BNPP_ERR_UNSUPPORTED, msg);
+            plans.back() = std::move(cp);
+        } else if (need(plans.back()) > budget) {
+            // every forward message does not fit: recompute them from checkpoints
+            // (chain-shaped trees), with as many checkpoint slots as fit
+            std::string msg;
+            VEPlan best;
+            int lo = 1, hi = 64, best_s = 0;
+            while (lo <= hi) {
+                int mid = (lo + hi) / 2;
+                VEPlan cp;
+                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, cp, &msg)) break;
+                if (need(cp) <= budget) {
+                    best_s = mid;
+                    best = std::move(cp);
+                    lo = mid + 1;
+                } else {
+                    hi = mid - 1;
+                }
+            }
+            if (best_s > 0) {
+                if (std::getenv("BNPP_TIMING")) std::fprintf(stderr, "[bnpp] bucket tree: %d checkpoint slots\n", best_s);
+                plans.back() = std::move(best);
+            }
+        }
     } else {
         // one independent VE per target (model.cpp:326-334), planned in parallel
         plans.resize(targets.size());
@@ -219,10 +251,10 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     int width = 0;
     const bool timing = std::getenv("BNPP_TIMING") != nullptr;
     double t0 = now_ms();
-    int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width);
+    const int eb = dtype == BNPP_F32 ? 4 : 8;
+    int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width, budget, eb);
     if (rc) return rc;
     if (timing) std::fprintf(stderr, "[bnpp] plans %.1f ms\n", now_ms() - t0);
-    const int eb = dtype == BNPP_F32 ? 4 : 8;
     std::vector<int64_t> src_sizes;
     for (auto &v : d.values) src_sizes.push_back((int64_t)v.size());
     std::vector<std::vector<const VEPlan *>> batches(1);
@@ -231,8 +263,8 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
         int64_t need = plan_peak_bytes(p, eb) + (int64_t)p.buckets.size() * 512;
         if (kind == 3 && need > budget) {
             char m[256];
-            std::snprintf(m, sizeof m, "bucket-tree marginals need %.2f GB of messages, budget %.2f GB "
-                          "(per-target marginals or a narrower order)", need / 1e9, budget / 1e9);
+            std::snprintf(m, sizeof m, "bucket-tree marginals need %.2f GB, budget %.2f GB: the tree is not a "
+                          "chain or no checkpoint count fits (per-target marginals or a narrower order)", need / 1e9, budget / 1e9);
             return set_err(BNPP_ERR_OOM, m);
         }
         if (!batches.back().empty() && acc + need > budget) {
@@ -275,7 +307,7 @@ int64_t memory_budget(bnpp_ctx *ctx) {
     if (ctx) {
         size_t fr = 0, tot = 0;
         (void)hipSetDevice(ctx->c.device);
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) return (int64_t)(fr * 0.6);
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) return (int64_t)(fr * 0.85);
     }
     return (int64_t)64e9;
 }

@@ -298,6 +298,8 @@ struct PlanBuilder {
     bool canonical;
     std::vector<int> rank;
     std::vector<int> level;                 // per table
+    bool sequential = false;                // every bucket one level after the previous (program order)
+    int last_level = 0;
 
     PlanBuilder(const std::vector<int> &c, VEPlan &plan, const std::vector<View> &sources,
                 const std::vector<int> &order, bool canon_layout)
@@ -344,9 +346,10 @@ struct PlanBuilder {
         b.elim_var = x;
         b.out_vars = ov;
         b.out_table = new_msg(ov);
-        int lv = 0;
+        int lv = sequential ? last_level : 0;
         for (const View &v : in) lv = std::max(lv, level[v.table]);
         b.level = lv + 1;
+        last_level = std::max(last_level, b.level);
         level[b.out_table] = b.level;
         p.entries += entries_of(in);
         p.elems_moved += moved_of(in, b.out_table);
@@ -497,6 +500,155 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
     }
     B.finish();
     return p;
+}
+
+// ------------------------------------------- chain bucket tree, checkpointed
+namespace {
+int64_t binom_capped(int n, int k) {             // C(n, k), saturating at 2^40
+    if (k < 0 || k > n) return 0;
+    k = std::min(k, n - k);
+    double r = 1;
+    for (int i = 1; i <= k; ++i) {
+        r = r * (n - k + i) / i;
+        if (r > 1099511627776.0) return (int64_t)1 << 40;
+    }
+    return (int64_t)(r + 0.5);
+}
+}  // namespace
+
+bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
+                            const std::vector<int> &order, const std::vector<int> &targets, int slots,
+                            VEPlan &out, std::string *msg) {
+    VEPlan p;
+    PlanBuilder B(cards, p, sources, order, true);
+    B.sequential = true;
+    const int nord = (int)order.size();
+    // symbolic forward pass: bucket contents, message scopes, tree shape
+    std::vector<std::vector<View>> src_in(nord);
+    std::vector<int> child(nord, -1), parent(nord, -1);
+    std::vector<char> has(nord, 0);
+    std::vector<std::vector<int>> lam_vars(nord);
+    for (const View &sv : sources) {
+        int bi = B.first_bucket(sv.vars, 0);
+        if (bi >= 0) src_in[bi].push_back(sv);
+    }
+    for (int i = 0; i < nord; ++i) {
+        std::vector<View> in = src_in[i];
+        if (child[i] >= 0) in.push_back(natural_view(0, lam_vars[child[i]], cards));
+        if (in.empty()) continue;
+        has[i] = 1;
+        lam_vars[i] = B.canon(remove_var(chain_scope(in), order[i]));
+        int par = B.first_bucket(lam_vars[i], i + 1);
+        parent[i] = par;
+        if (par >= 0) {
+            if (child[par] >= 0) {
+                if (msg) *msg = "bucket tree is not a chain (a bucket has two children)";
+                return false;
+            }
+            child[par] = i;
+        }
+    }
+    std::vector<int> result_of(cards.size(), -1);
+    // the forward message of bucket i from its child's message (or none)
+    auto forward = [&](int i, const View *lam_child) {
+        std::vector<View> in = src_in[i];
+        if (lam_child) in.push_back(*lam_child);
+        return B.view(B.emit(in, order[i], false));
+    };
+    auto reduce_to = [&](std::vector<View> in, int t) {
+        std::vector<int> y;
+        for (int v : chain_scope(in))
+            if (v != t) y.push_back(v);
+        std::sort(y.begin(), y.end(), [&](int a, int b) { return B.rank[a] < B.rank[b]; });
+        if (y.empty()) return B.emit(in, -1, false);
+        int tb = B.emit(in, y[0], false);
+        for (size_t j = 1; j < y.size(); ++j) tb = B.emit({B.view(tb)}, y[j], false);
+        return tb;
+    };
+    for (int top = 0; top < nord; ++top) {
+        if (!has[top] || parent[top] >= 0) continue;
+        std::vector<int> path;                       // leaf ... root (child -> parent)
+        for (int b = top; b >= 0; b = child[b]) path.push_back(b);
+        std::reverse(path.begin(), path.end());
+        const int m = (int)path.size();
+        // backward sweep state: pi of path[j] (message from path[j+1] into path[j])
+        View pi_cur;
+        bool have_pi = false;                        // pi of the root: constant 1
+        int next_deliver = m - 2;
+        // deliver(j): lam_j is live.  pi_j = sum F_{j+1} * pi_{j+1} down to sep_j;
+        // marginal of x_{j+1} = lam_j * pi_j summed down to x_{j+1}
+        auto deliver = [&](int j, const View &lam_j) {
+            if (j != next_deliver) return false;
+            const int q = path[j + 1];
+            std::vector<View> in = src_in[q];
+            if (have_pi) in.push_back(pi_cur);
+            View pij;
+            bool hp = false;
+            if (!in.empty()) {
+                std::vector<int> y;
+                for (int v : chain_scope(in))
+                    if (std::find(lam_j.vars.begin(), lam_j.vars.end(), v) == lam_j.vars.end()) y.push_back(v);
+                std::sort(y.begin(), y.end(), [&](int a, int b) { return B.rank[a] < B.rank[b]; });
+                if (y.empty() && in.size() == 1) {
+                    pij = in[0];
+                } else {
+                    int tb = B.emit(in, y.empty() ? -1 : y[0], false);
+                    for (size_t k = 1; k < y.size(); ++k) tb = B.emit({B.view(tb)}, y[k], false);
+                    pij = B.view(tb);
+                }
+                hp = true;
+            }
+            std::vector<View> bel{lam_j};
+            if (hp) bel.push_back(pij);
+            result_of[order[q]] = reduce_to(bel, order[q]);
+            pi_cur = pij;
+            have_pi = hp;
+            --next_deliver;
+            return true;
+        };
+        // reverse(lo, hi, start, s): deliver j = hi-1 ... lo; `start` = lam_{lo-1}
+        // (null for lo == 0), s free checkpoint slots (binomial checkpointing)
+        bool ok = true;
+        std::function<void(int, int, const View *, int)> reverse = [&](int lo, int hi, const View *start, int sl) {
+            const int len = hi - lo;
+            if (len <= 0 || !ok) return;
+            if (len == 1 || sl <= 0) {
+                for (int j = hi - 1; j >= lo; --j) {          // stream lam_lo..lam_j, deliver lam_j
+                    View cur = forward(path[lo], start);
+                    for (int k = lo + 1; k <= j; ++k) cur = forward(path[k], &cur);
+                    ok = ok && deliver(j, cur);
+                }
+                return;
+            }
+            int r = 1;                                         // repetitions needed with sl slots
+            while (binom_capped(sl + r, sl) < len) ++r;
+            int64_t right_cap = binom_capped(sl - 1 + r, sl - 1);
+            int d = (int)std::max<int64_t>(1, len - std::min<int64_t>(right_cap, len - 1));
+            View ck = forward(path[lo], start);                // advance d steps, keep lam_{lo+d-1}
+            for (int k = lo + 1; k < lo + d; ++k) ck = forward(path[k], &ck);
+            const int c = lo + d - 1;
+            reverse(c + 1, hi, &ck, sl - 1);
+            ok = ok && deliver(c, ck);
+            reverse(lo, c, start, sl);
+        };
+        reverse(0, m - 1, nullptr, slots);
+        if (!ok || next_deliver != -1) {
+            if (msg) *msg = "internal: checkpoint schedule out of order";
+            return false;
+        }
+        // the leaf's marginal: its own bucket with the message from above
+        std::vector<View> bel = src_in[path[0]];
+        if (have_pi) bel.push_back(pi_cur);
+        result_of[order[path[0]]] = reduce_to(bel, order[path[0]]);
+    }
+    for (int t : targets) {
+        int r = t >= 0 && t < (int)cards.size() ? result_of[t] : -1;
+        p.results.push_back(r);
+        p.results_vars.push_back(r >= 0 ? p.msgs[r - p.n_src].vars : std::vector<int>{});
+    }
+    B.finish();
+    out = std::move(p);
+    return true;
 }
 
 int64_t plan_peak_bytes(const VEPlan &p, int elem_bytes) {

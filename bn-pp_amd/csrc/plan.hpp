@@ -90,6 +90,15 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
 VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &sources,
                         const std::vector<int> &order, const std::vector<int> &targets);
 
+// The same marginals in bounded memory when the bucket tree is a chain (a
+// column-sweep order on a grid): forward messages are recomputed from `slots`
+// checkpoints by binomial checkpointing (revolve), buckets run in program order
+// (one level each) so the arena holds about slots + 5 messages.  Returns false
+// (msg) when the tree is not a chain.
+bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
+                            const std::vector<int> &order, const std::vector<int> &targets, int slots,
+                            VEPlan &out, std::string *msg);
+
 // Flattened, level-ordered launch schedule over one or more plans sharing the
 // same sources.  Tables: [0, n_src) sources, then every plan's messages.
 struct Schedule {

@@ -124,3 +124,34 @@ def test_tree_job_relaunch(ctx):
     job.launch()
     assert job.results() == a
     job.close()
+
+
+@pytest.mark.parametrize("slots", [1, 2, 3, 7, 64])
+def test_tree_chain_checkpointed_matches(ctx, slots):
+    """Chain-shaped bucket tree (column sweep) with forward messages recomputed
+    from `slots` checkpoints (binomial checkpointing; 1 slot degenerates to
+    quadratic recomputation): same marginals as the per-target engine."""
+    m = bnpp.Model.from_dict(synth.ising_grid(6, 9, seed=11))
+    col = [r * 9 + c for c in range(9) for r in range(6)]
+    ev = {13: 1}
+    want, _ = bnpp.marginals(ctx, m, ev, "mf", bnpp.F64)
+    os.environ["BNPP_TREE_SLOTS"] = str(slots)
+    try:
+        got, _ = bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F64, order=col)
+        got32, _ = bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F32, order=col)
+    finally:
+        del os.environ["BNPP_TREE_SLOTS"]
+    for t in range(m.n_vars):
+        assert _close(got[t], want[t], 1e-12), (slots, t, got[t], want[t])
+        assert _close(got32[t], want[t], 1e-5), (slots, t, got32[t], want[t])
+
+
+def test_tree_chain_mode_rejects_non_chain(ctx):
+    m = bnpp.Model.load(model_path("alarm.uai"))
+    os.environ["BNPP_TREE_SLOTS"] = "4"
+    try:
+        with pytest.raises(bnpp.BnppError) as e:
+            bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64)
+        assert e.value.status == bnpp.ERR_UNSUPPORTED
+    finally:
+        del os.environ["BNPP_TREE_SLOTS"]

@@ -150,3 +150,24 @@ def test_bucket_tree_rejects_null_context():
     with pytest.raises(bnpp.BnppError) as e:
         bnpp.marginals_tree(null_ctx, m)
     assert e.value.status == bnpp.ERR_INVALID
+
+
+def test_plan_stats_checkpointed_chain():
+    """Column-sweep grids give chain-shaped bucket trees: with few checkpoint
+    slots the plan recomputes forward messages (more entries) and runs in
+    program order (one bucket per level)."""
+    import os
+    m = bnpp.Model.load(model_path("ising10x10.uai"))
+    col = [r * 10 + c for c in range(10) for r in range(10)]
+    full = bnpp.plan_stats(m, 3, {}, "mf", order=col)
+    os.environ["BNPP_TREE_SLOTS"] = "2"
+    try:
+        ck = bnpp.plan_stats(m, 3, {}, "mf", order=col)
+        with pytest.raises(bnpp.BnppError) as e:     # min-fill on alarm: not a chain
+            bnpp.plan_stats(bnpp.Model.load(model_path("alarm.uai")), 3, {}, "mf")
+        assert e.value.status == bnpp.ERR_UNSUPPORTED
+    finally:
+        del os.environ["BNPP_TREE_SLOTS"]
+    assert ck[0] > full[0]                           # recomputation
+    assert ck[2] == ck[3]                            # one bucket per level
+    assert ck[1] < full[1]                           # smaller arena
