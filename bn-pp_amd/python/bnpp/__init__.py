@@ -18,6 +18,13 @@ if os.environ.get("BNPP_LIB"):          # A/B of alternative builds (experiments
 if not os.path.exists(LIB_PATH):
     raise ImportError("libbnpp.so not built (%s); run `make -C bn-pp_amd` or __graft_entry__.build()" % LIB_PATH)
 
+# One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.  When it
+# is installed, load it first so libbnpp binds to that same runtime (with two
+# runtimes in one process, whichever initialises second sees no device).
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
 _lib = C.CDLL(LIB_PATH)
 
 OK, ERR_INVALID, ERR_NO_DEVICE, ERR_OOM, ERR_HIP, ERR_IO, ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6

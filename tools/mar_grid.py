@@ -27,10 +27,17 @@ def main():
     from bnpp import synth
     r, c = args.rows, args.cols
     dt = bnpp.F32 if args.dtype == "f32" else bnpp.F64
+    import torch                                           # initialise torch's HIP runtime first
+    free, _ = torch.cuda.mem_get_info(0)
     ctx = bnpp.Context(0)
     m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=args.seed))
     col = [rr * c + cc for cc in range(c) for rr in range(r)]
-    st = bnpp.plan_stats(m, 3, {}, "mf", dtype=dt, order=col)
+    if "BNPP_MEM_BUDGET_GB" not in os.environ:             # host-only stats: size them like the device run
+        os.environ["BNPP_MEM_BUDGET_GB"] = str(free * 0.85 / 1e9)
+        st = bnpp.plan_stats(m, 3, {}, "mf", dtype=dt, order=col)
+        del os.environ["BNPP_MEM_BUDGET_GB"]
+    else:
+        st = bnpp.plan_stats(m, 3, {}, "mf", dtype=dt, order=col)
     pr_st = bnpp.plan_stats(m, 0, {}, "mf", dtype=dt, order=col)
     print(json.dumps({"phase": "plan", "tree_entries": st[0], "pr_entries": pr_st[0], "arena_GB": st[1] / 1e9,
                       "buckets": st[3], "alg_GB": st[6] / 1e9, "width": st[4]}), flush=True)
