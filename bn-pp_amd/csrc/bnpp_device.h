@@ -70,7 +70,8 @@ struct LevelArgs {
 };
 
 // loads of the big input of a stream bucket, relative to one thread's tile
-enum BigClass : int32_t { kBigRow = 1, kBigCol = 2, kBigFull = 3, kBigDirect = 4, kBigOne = 5 };
+enum BigClass : int32_t { kBigRow = 1, kBigCol = 2, kBigFull = 3, kBigDirect = 4, kBigOne = 5,
+                                kBigInter2 = 6, kBigInter4 = 7 };   // summed var fastest in the big input, card 2 / 4
 constexpr int kStreamSmallMax = 4096;      // entries: inputs at most this big go to LDS
 constexpr int kStreamLdsBudget = 32768;    // bytes of LDS for the small inputs
 

@@ -434,7 +434,7 @@ __global__ __launch_bounds__(kBlock) void bucket_single_kernel(const SingleArgs 
 template <typename T, int V1, int V2, int BC>
 struct BigTile {
     static constexpr int TS = V1 * V2;
-    static constexpr int N = BC == kBigRow ? V1 : BC == kBigCol ? V2 : BC == kBigOne ? 1 : TS;
+    static constexpr int N = BC == kBigRow ? V1 : BC == kBigCol ? V2 : (BC == kBigOne || BC >= kBigInter2) ? 1 : TS;
     static __device__ __forceinline__ void issue(const T *src, int64_t s0, int64_t s1, T (&buf)[N]) {
         if constexpr (BC == kBigOne) {
             buf[0] = src[0];
@@ -520,56 +520,115 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
         }
     }
 
+    // every small input (from LDS) into the product, in chain order around the
+    // big one (interleaved path; the streamed path below keeps it inline)
+    auto smalls = [&](int v, T (&p)[TS], auto &&big_apply) {
+#pragma unroll
+        for (int i = 0; i < kStreamMaxIn; ++i) {
+            if (i >= b.n_in) break;                         // uniform
+            if (i == st.big) {
+                big_apply(p);
+            } else {
+                // small input from LDS, read once per distinct entry of the tile
+                const T *t = small + rel[i] + v * (int32_t)b.es[i];
+                const int32_t s0 = (int32_t)b.s0[i], s1 = (int32_t)b.s1[i];
+                if (s0 == 0 && s1 == 0) {
+                    const T y = t[0];
+#pragma unroll
+                    for (int j = 0; j < TS; ++j) p[j] = p[j] * y;
+                } else if (s1 == 0) {
+                    T y[V1];
+#pragma unroll
+                    for (int j1 = 0; j1 < V1; ++j1) y[j1] = t[j1 * s0];
+#pragma unroll
+                    for (int j = 0; j < TS; ++j) p[j] = p[j] * y[j % V1];
+                } else if (s0 == 0) {
+                    T y[V2];
+#pragma unroll
+                    for (int j2 = 0; j2 < V2; ++j2) y[j2] = t[j2 * s1];
+#pragma unroll
+                    for (int j = 0; j < TS; ++j) p[j] = p[j] * y[j / V1];
+                } else {
+#pragma unroll
+                    for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+                        for (int j1 = 0; j1 < V1; ++j1) p[j2 * V1 + j1] = p[j2 * V1 + j1] * t[j1 * s0 + j2 * s1];
+                }
+            }
+        }
+    };
 #pragma unroll
     for (int j = 0; j < TS; ++j) acc[j] = T(0);
-    constexpr int U = 4;
-    for (int v0 = 0; v0 < b.k; v0 += U) {
-        T bb[U][BT::N];
+    if constexpr (BC == kBigInter2 || BC == kBigInter4) {
+        // the summed variable is the big input's fastest dim and the tile's
+        // dim 0 follows it: the tile's big entries for every v are V1*K
+        // contiguous values, fetched by one vector load (V2 == 1)
+        constexpr int K = BC == kBigInter2 ? 2 : 4;
+        T all[V1 * K];
+        load_n<T, V1 * K, kNtLoad>(bsrc, all);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (v0 + u < b.k) BT::issue(bsrc + (int64_t)(v0 + u) * bes, bs0, bs1, bb[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int v = v0 + u;
-            if (v >= b.k) break;                                // uniform
+        for (int v = 0; v < K; ++v) {
             T p[TS];
 #pragma unroll
             for (int j = 0; j < TS; ++j) p[j] = T(1);
+            smalls(v, p, [&](T (&q)[TS]) {
 #pragma unroll
-            for (int i = 0; i < kStreamMaxIn; ++i) {
-                if (i >= b.n_in) break;                         // uniform
-                if (i == st.big) {
-                    BT::apply(bb[u], p);
-                } else {
-                    // small input from LDS, read once per distinct entry of the tile
-                    const T *t = small + rel[i] + v * (int32_t)b.es[i];
-                    const int32_t s0 = (int32_t)b.s0[i], s1 = (int32_t)b.s1[i];
-                    if (s0 == 0 && s1 == 0) {
-                        const T y = t[0];
-#pragma unroll
-                        for (int j = 0; j < TS; ++j) p[j] = p[j] * y;
-                    } else if (s1 == 0) {
-                        T y[V1];
-#pragma unroll
-                        for (int j1 = 0; j1 < V1; ++j1) y[j1] = t[j1 * s0];
-#pragma unroll
-                        for (int j = 0; j < TS; ++j) p[j] = p[j] * y[j % V1];
-                    } else if (s0 == 0) {
-                        T y[V2];
-#pragma unroll
-                        for (int j2 = 0; j2 < V2; ++j2) y[j2] = t[j2 * s1];
-#pragma unroll
-                        for (int j = 0; j < TS; ++j) p[j] = p[j] * y[j / V1];
-                    } else {
-#pragma unroll
-                        for (int j2 = 0; j2 < V2; ++j2)
-#pragma unroll
-                            for (int j1 = 0; j1 < V1; ++j1) p[j2 * V1 + j1] = p[j2 * V1 + j1] * t[j1 * s0 + j2 * s1];
-                    }
-                }
-            }
+                for (int j = 0; j < TS; ++j) q[j] = q[j] * all[j * K + v];
+            });
 #pragma unroll
             for (int j = 0; j < TS; ++j) acc[j] = acc[j] + p[j];
+        }
+    } else {
+        constexpr int U = 4;
+        for (int v0 = 0; v0 < b.k; v0 += U) {
+            T bb[U][BT::N];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (v0 + u < b.k) BT::issue(bsrc + (int64_t)(v0 + u) * bes, bs0, bs1, bb[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int v = v0 + u;
+                if (v >= b.k) break;                                // uniform
+                T p[TS];
+#pragma unroll
+                for (int j = 0; j < TS; ++j) p[j] = T(1);
+#pragma unroll
+                for (int i = 0; i < kStreamMaxIn; ++i) {
+                    if (i >= b.n_in) break;                         // uniform
+                    if (i == st.big) {
+                        BT::apply(bb[u], p);
+                    } else {
+                        // small input from LDS, read once per distinct entry of the tile
+                        const T *t = small + rel[i] + v * (int32_t)b.es[i];
+                        const int32_t s0 = (int32_t)b.s0[i], s1 = (int32_t)b.s1[i];
+                        if (s0 == 0 && s1 == 0) {
+                            const T y = t[0];
+#pragma unroll
+                            for (int j = 0; j < TS; ++j) p[j] = p[j] * y;
+                        } else if (s1 == 0) {
+                            T y[V1];
+#pragma unroll
+                            for (int j1 = 0; j1 < V1; ++j1) y[j1] = t[j1 * s0];
+#pragma unroll
+                            for (int j = 0; j < TS; ++j) p[j] = p[j] * y[j % V1];
+                        } else if (s0 == 0) {
+                            T y[V2];
+#pragma unroll
+                            for (int j2 = 0; j2 < V2; ++j2) y[j2] = t[j2 * s1];
+#pragma unroll
+                            for (int j = 0; j < TS; ++j) p[j] = p[j] * y[j / V1];
+                        } else {
+#pragma unroll
+                            for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+                                for (int j1 = 0; j1 < V1; ++j1)
+                                    p[j2 * V1 + j1] = p[j2 * V1 + j1] * t[j1 * s0 + j2 * s1];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < TS; ++j) acc[j] = acc[j] + p[j];
+            }
         }
     }
     if (b.flags & kScale) {
@@ -734,10 +793,11 @@ static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_
 }
 
 #define BNPP_STREAM_BC(X, T, V1, V2) X(T, V1, V2, 1) X(T, V1, V2, 2) X(T, V1, V2, 3) X(T, V1, V2, 4) X(T, V1, V2, 5)
-#define BNPP_STREAM_F32(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
+#define BNPP_STREAM_INTER(X, T) X(T, 2, 1, 6) X(T, 4, 1, 6) X(T, 2, 1, 7) X(T, 4, 1, 7)
+#define BNPP_STREAM_F32(X, T) BNPP_STREAM_INTER(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
     BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2) BNPP_STREAM_BC(X, T, 4, 4) \
     BNPP_STREAM_BC(X, T, 2, 8)
-#define BNPP_STREAM_F64(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
+#define BNPP_STREAM_F64(X, T) BNPP_STREAM_INTER(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
     BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2)
 #define BNPP_CASE_SLEVEL(T, V1, V2, BC) \
     case 4096 + BC * 64 + V1 * 8 + V2: return go_stream_level<T, V1, V2, BC>(a, small_elems, max_grid, stream);

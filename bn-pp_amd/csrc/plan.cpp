@@ -259,8 +259,24 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 d.n_tiles = out_size / v1;
                 divisor(merged.size() < 2 ? 1 : merged[1].card, d.tdiv1);
             }
+            // interleaved: the summed variable is the big input's fastest dim and
+            // output dim 0 follows it, so a V1-entry tile reads V1*k contiguous values
+            bool inter = false;
+            if ((k == 2 || k == 4) && es[big] == 1 && s0 == k && v1 >= 2 && !merged.empty()) {
+                const int64_t vw = 16 / eb;
+                inter = b.in[big].base % vw == 0 && (int64_t)(v1 * k) % vw == 0;
+                for (size_t j = 1; inter && j < merged.size(); ++j)
+                    if (merged[j].s[big] % vw) inter = false;
+                if (inter && v2 > 1) {
+                    v2 = 1;
+                    d.v2 = 1;
+                    d.n_tiles = out_size / v1;
+                    divisor(merged.size() < 2 ? 1 : merged[1].card, d.tdiv1);
+                }
+            }
             int bc;
-            if (s0 == 0 && (v2 == 1 || s1 == 0)) bc = kBigOne;
+            if (inter) bc = k == 2 ? kBigInter2 : kBigInter4;
+            else if (s0 == 0 && (v2 == 1 || s1 == 0)) bc = kBigOne;
             else if (v1 > 1 && s0 == 1 && (v2 == 1 || s1 == 0)) bc = kBigRow;
             else if (v2 > 1 && s0 == 0 && s1 == 1) bc = kBigCol;
             else if (v1 > 1 && v2 > 1 && s0 == 1 && s1 == v1) bc = kBigFull;
@@ -293,7 +309,8 @@ namespace {
 // Emits buckets and message tables into a VEPlan (shared by plan_ve and
 // plan_bucket_tree).  Levels: a bucket runs one level after its latest input.
 struct PlanBuilder {
-    const std::vector<int> &cards;
+    std::vector<int> cards;                 // model cards + virtual composite variables
+    int n_real = 0;
     VEPlan &p;
     bool canonical;
     std::vector<int> rank;
@@ -303,7 +320,7 @@ struct PlanBuilder {
 
     PlanBuilder(const std::vector<int> &c, VEPlan &plan, const std::vector<View> &sources,
                 const std::vector<int> &order, bool canon_layout)
-        : cards(c), p(plan), canonical(canon_layout) {
+        : cards(c), n_real((int)c.size()), p(plan), canonical(canon_layout) {
         p.n_src = (int)sources.size();
         rank.assign(cards.size(), -1);
         for (int i = (int)order.size() - 1; i >= 0; --i) rank[order[i]] = i;
@@ -384,7 +401,84 @@ struct PlanBuilder {
         }
         return best;
     }
+    // Merge variables `g` (slow to fast) into one virtual variable in every
+    // input: each input must hold all of them as one contiguous mixed-radix
+    // block in that order, or none.  Returns the virtual id, or -1.
+    int merge_group(std::vector<View> &in, const std::vector<int> &g) {
+        if (g.empty()) return -1;
+        int64_t prod = 1;
+        for (int v : g) prod *= cards[v];
+        if (prod > (int64_t)INT32_MAX) return -1;
+        std::vector<View> out = in;
+        for (View &w : out) {
+            std::vector<int> pos;
+            for (int v : g) {
+                auto it = std::find(w.vars.begin(), w.vars.end(), v);
+                pos.push_back(it == w.vars.end() ? -1 : (int)(it - w.vars.begin()));
+            }
+            int present = 0;
+            for (int q : pos) present += q >= 0;
+            if (present == 0) continue;
+            if (present != (int)g.size()) return -1;
+            for (size_t k = 0; k + 1 < g.size(); ++k)
+                if (w.strides[pos[k]] != w.strides[pos[k + 1]] * cards[g[k + 1]]) return -1;
+            const int64_t fast = w.strides[pos.back()];
+            View nw;
+            nw.table = w.table;
+            nw.base = w.base;
+            for (size_t j = 0; j < w.vars.size(); ++j)
+                if (std::find(g.begin(), g.end(), w.vars[j]) == g.end()) {
+                    nw.vars.push_back(w.vars[j]);
+                    nw.strides.push_back(w.strides[j]);
+                }
+            nw.vars.push_back((int)cards.size());
+            nw.strides.push_back(fast);
+            w = nw;
+        }
+        cards.push_back((int)prod);
+        rank.push_back(-1);
+        in.swap(out);
+        return (int)cards.size() - 1;
+    }
+    // Sum everything in `in` except `t` down to a table over {t}.  When the
+    // summed variables are contiguous in every input (messages in canonical
+    // layout, t slowest), they are summed in a few composite passes of
+    // <= ~2K values each (about one read of the inputs); otherwise one
+    // variable at a time in elimination-rank order.
+    int reduce_to(std::vector<View> in, int t) {
+        std::vector<int> y;
+        for (int v : chain_scope(in))
+            if (v != t) y.push_back(v);
+        std::sort(y.begin(), y.end(), [&](int a, int b) { return rank[a] < rank[b]; });
+        if (y.empty()) return emit(in, -1, false);
+        while (!y.empty()) {
+            int64_t P = 1;
+            for (int v : y) P *= cards[v];
+            // one stage sums kk values per output: up to 2048 while the output
+            // keeps >= 2^20 entries, else 32 (small stages stay parallel)
+            int64_t kk = P > ((int64_t)1 << 22) ? std::min<int64_t>(2048, P >> 20) : std::min<int64_t>(P, 32);
+            int64_t want_lo = std::max<int64_t>(1, P / kk);
+            size_t cut = y.size();
+            int64_t lo = 1;
+            while (cut > 0 && lo * cards[y[cut - 1]] <= want_lo) lo *= cards[y[--cut]];
+            if (cut == 0) cut = 1;
+            std::vector<int> g(y.begin(), y.begin() + cut);
+            std::vector<View> merged = in;
+            int vv = g.size() >= 2 ? merge_group(merged, g) : -1;
+            int tb;
+            if (vv >= 0) {
+                tb = emit(merged, vv, false);
+                y.erase(y.begin(), y.begin() + cut);
+            } else {
+                tb = emit(in, y[0], false);
+                y.erase(y.begin());
+            }
+            in = {view(tb)};
+        }
+        return in[0].table;
+    }
     void finish() {
+        if ((int)cards.size() > n_real) p.cards_ext = cards;
         std::stable_sort(p.buckets.begin(), p.buckets.end(),
                          [](const BucketSpec &a, const BucketSpec &b) { return a.level < b.level; });
         p.n_levels = p.buckets.empty() ? 0 : p.buckets.back().level;
@@ -494,9 +588,9 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
                 best_size = sz;
             }
         }
-        View r = reduce(best, {t}, true);
-        p.results.push_back(r.table);
-        p.results_vars.push_back(r.vars);
+        int rt = B.reduce_to(best, t);
+        p.results.push_back(rt);
+        p.results_vars.push_back(p.msgs[rt - p.n_src].vars);
     }
     B.finish();
     return p;
@@ -555,16 +649,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         if (lam_child) in.push_back(*lam_child);
         return B.view(B.emit(in, order[i], false));
     };
-    auto reduce_to = [&](std::vector<View> in, int t) {
-        std::vector<int> y;
-        for (int v : chain_scope(in))
-            if (v != t) y.push_back(v);
-        std::sort(y.begin(), y.end(), [&](int a, int b) { return B.rank[a] < B.rank[b]; });
-        if (y.empty()) return B.emit(in, -1, false);
-        int tb = B.emit(in, y[0], false);
-        for (size_t j = 1; j < y.size(); ++j) tb = B.emit({B.view(tb)}, y[j], false);
-        return tb;
-    };
+    auto reduce_to = [&](std::vector<View> in, int t) { return B.reduce_to(std::move(in), t); };
     for (int top = 0; top < nord; ++top) {
         if (!has[top] || parent[top] >= 0) continue;
         std::vector<int> path;                       // leaf ... root (child -> parent)
@@ -803,7 +888,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         BucketSpec b = *it.b;
         for (View &v : b.in) v.table = remap(it.plan, v.table);
         b.out_table = remap(it.plan, b.out_table);
-        it.ok = build_desc(b, cards, max_vec, it.d, it.pool, &it.msg);
+        const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
+        it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
         it.key = it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2) : variant_key(it.d.n_in, it.d.v1, it.d.v2);
     });
     for (const Item &it : items)

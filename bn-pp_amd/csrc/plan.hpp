@@ -66,6 +66,9 @@ struct VEPlan {
     // no table (evidence / variable in no factor); replaces result_table
     std::vector<int> results;
     std::vector<std::vector<int>> results_vars;
+    // cards of the model followed by virtual (composite) variables the plan
+    // sums in one pass; empty: the model's cards
+    std::vector<int> cards_ext;
     int64_t max_table = 0;              // largest message entries
     double entries = 0;                 // sum over buckets of prod(card) over the union scope
     double elems_moved = 0;             // sum over buckets of (|inputs| + |output|): algorithmic traffic

@@ -144,6 +144,35 @@ def test_random_buckets_bit_exact_vs_oracle(ctx):
         assert vals == ref.values, it
 
 
+@pytest.mark.parametrize("k,n_other", [(2, 12), (4, 6), (2, 9)])
+def test_interleaved_stream_buckets(ctx, k, n_other):
+    """Stream form with the summed variable as the big input's FASTEST dim and
+    the output's dim 0 right above it (the backward messages of a column-sweep
+    bucket tree): bit-exact against the oracle in fp64, 1e-6 in fp32."""
+    rng = random.Random(k * 100 + n_other)
+    y = 0
+    others = list(range(1, n_other + 2))
+    cards = {y: k}
+    for v in others:
+        cards[v] = rng.choice([2, 3, 4])
+    cards[others[-1]] = 4                     # output dim 0: a multiple of the tile width
+    big_scope = others + [y]
+    size = 1
+    for v in big_scope:
+        size *= cards[v]
+    big = (big_scope, [rng.uniform(0.5, 2.0) for _ in range(size)])
+    pair = ([others[-1], y], [rng.uniform(0.5, 2.0) for _ in range(4 * k)])
+    unary = ([y], [rng.uniform(0.5, 2.0) for _ in range(k)])
+    for ins in ([big, pair], [pair, big, unary], [unary, big]):
+        fs = [refcpu.Factor.new(sc, cards, v) for sc, v in ins]
+        ref = refcpu.bucket(fs, y, cards[y])
+        scope, vals = run_bucket(ctx, bnpp.F64, cards, ins, y)
+        assert scope == ref.scope
+        assert vals == ref.values
+        scope, vals = run_bucket(ctx, bnpp.F32, cards, ins, y)
+        assert max(abs(a - b) / abs(b) for a, b in zip(vals, ref.values)) < 1e-6
+
+
 def test_permuted_output_layout(ctx):
     """Any permutation of the output scope is accepted and gives the same table, transposed."""
     rng = random.Random(5)
