@@ -15,6 +15,14 @@ events, same stream) against 8.0 TB/s.  CPU baseline: the reference's own
 Factor::product + Factor::sum_out (oracle/_ref/ref_harness micro, compiled from
 the reference sources), or the oracle restatement if that binary is absent,
 single core, on a bounded sample of the same bucket shape.
+
+"mar": the metric's second half on its own instance -- all marginals of the
+32x32 Ising grid UAI (BASELINE config 3) through the checkpointed two-pass
+bucket tree (column-sweep order, width 32, fp32), split over the ranks by
+chain segments; wall-clock like the reference's uptime.  The reference cannot
+run this instance (min-fill width 46), so its time is bounded from below by
+n_vars x the column-sweep PR's factor-entries at the measured cpu_baseline
+rate.  "secondary": 12x12 (reference-runnable, measured reference time).
 """
 import argparse
 import json
@@ -48,45 +56,56 @@ def cpu_baseline(k: int, w_cpu: int, reps: int):
             "sample": sample + " (oracle restatement)", "seconds": sec}
 
 
-def mar_wallclock(ctx, rank, world, dist, dev, rows=12, cols=12):
-    """Second half of the metric: MAR wall-clock (BASELINE config 3 restated to
-    the largest reference-runnable square grid).  All marginals of
-    an R x C Ising grid via VE with min-fill (BN::marginals, model.cpp:303-346),
-    fp64; targets dealt round-robin over ranks and assembled with one
+def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_order, cpu_rate=None):
+    """Second half of the metric: MAR wall-clock.  All marginals of an R x C
+    Ising grid (BN::marginals, model.cpp:303-346) by the two-pass bucket tree
+    (bnpp_marginals_tree_part): on one GPU the whole tree; on N GPUs part r of
+    N (a contiguous segment of the chain: its forward prefix, the backward
+    messages down to it, checkpointed recomputation inside it), assembled by one
     all-reduce.  Timed like the reference's uptime (ordering + planning + device
-    run + normalize), max over ranks."""
+    run + normalise), max over ranks."""
     import torch
     import bnpp
     from bnpp import synth, dist as bdist
 
+    dt = bnpp.F32 if dtype_name == "f32" else bnpp.F64
     m = bnpp.Model.from_dict(synth.ising_grid(rows, cols, seed=0))
-
-    def compute(targets):
-        marg, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64, targets=targets)
-        return marg
-
-    compute([0])                                        # warm the code paths
+    order = [r * cols + c for c in range(cols) for r in range(rows)] if column_order else None
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    marg = bdist.sharded_marginals(m.n_vars, m.cards, rank, world, compute, dist)
+    marg = bdist.sharded_tree_marginals(ctx, m, rank, world, dist, {}, "mf", dt, order)
     ms = (time.perf_counter() - t0) * 1e3
     if dist is not None:
         tt = torch.tensor([ms], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         ms = tt.item()
-    ref_ms = None
+    name = "ising%dx%d" % (rows, cols)
+    rec = {"instance": "%s all marginals, bucket tree, %s order, %s" % (
+               name, "column-sweep (width %d)" % rows if column_order else "min-fill", dtype_name),
+           "wall_ms": ms, "n_gpus": world, "p_var0": marg[0],
+           "max_sum_err": max(abs(sum(p) - 1.0) for p in marg.values())}
     ref_file = os.path.join(REPO, "profiles", "r01_ve_bench.jsonl")
+    ref_ms = None
     if os.path.exists(ref_file):
         for line in open(ref_file):
             r = json.loads(line)
-            if r.get("instance") == "ising%dx%d" % (rows, cols) and r.get("task") == "MAR" and r.get("ref_ms"):
+            if r.get("instance") == name and r.get("task") == "MAR" and r.get("ref_ms"):
                 ref_ms = r["ref_ms"]
-    return {"instance": "ising%dx%d all marginals, min-fill, fp64 (config 3 restated)" % (rows, cols),
-            "wall_ms": ms, "n_gpus": world, "p_var0": marg[0],
-            "reference_cpu_ms": ref_ms,
-            "reference_cpu_source": "profiles/r01_ve_bench.jsonl (oracle/_ref ref_harness mar, 1 core of the GPU box)",
-            "speedup_vs_reference": (ref_ms / ms) if ref_ms else None}
+    if ref_ms:
+        rec.update({"reference_cpu_ms": ref_ms,
+                    "reference_cpu_source": "profiles/r01_ve_bench.jsonl (oracle/_ref ref_harness mar, 1 core)",
+                    "speedup_vs_reference": ref_ms / ms})
+    elif cpu_rate:
+        # the reference cannot run it (min-fill width 46 at 32x32); lower bound:
+        # one VE per variable, each at least the column-sweep PR's factor-entries,
+        # at the reference's measured product+sum-out rate on this host
+        pr = bnpp.plan_stats(m, 0, {}, "mf", dtype=dt, order=order)[0]
+        lb = m.n_vars * pr / cpu_rate
+        rec.update({"reference_cpu_lower_bound_s": lb, "speedup_vs_reference_lower_bound": lb * 1e3 / ms,
+                    "reference_note": "reference MAR = one VE per variable (model.cpp:326-334); bound = n_vars x "
+                                      "factor-entries of the width-%d column-sweep PR / measured cpu_baseline rate" % rows})
+    return rec
 
 
 def main():
@@ -98,9 +117,11 @@ def main():
     ap.add_argument("--w", type=int, default=14)
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
     ap.add_argument("--cpu-w", type=int, default=10, help="bucket width of the bounded CPU-baseline sample")
-    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-mar", action="store_true")
+    ap.add_argument("--mar-rows", type=int, default=32)
+    ap.add_argument("--mar-cols", type=int, default=32)
     args = ap.parse_args()
 
     import torch
@@ -166,9 +187,7 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3)
 
     # sanity: checksum of checksums (sum_out = sum_x rowsum(m)_x * rowsum(f)_x)
-    M = m_t.double().reshape(k, S)
-    F = f_t.double().reshape(k, k)
-    want = (M.sum(1) * F.sum(1)).sum().item()
+    want = (m_t.double().reshape(k, S).sum(1) * f_t.double().reshape(k, k).sum(1)).sum().item()
     got = out.double().sum().item()
     ok = abs(got - want) <= (1e-4 if dt == bnpp.F32 else 1e-9) * want
 
@@ -183,7 +202,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(k, args.cpu_w, args.cpu_reps)
 
-    mar = None if args.no_mar else mar_wallclock(ctx, rank, world, dist if world > 1 else None, dev)
+    mar = None
+    if not args.no_mar:
+        del m_t, f_t, out                                 # the 32x32 tree wants the HBM
+        torch.cuda.empty_cache()
+        d = dist if world > 1 else None
+        rate = cpu["value"] if cpu else 7.2e6             # profiles/r01_bench.json cpu_baseline when not run
+        mar = mar_wallclock(ctx, rank, world, d, dev, args.mar_rows, args.mar_cols, "f32", True, rate)
+        mar["secondary"] = mar_wallclock(ctx, rank, world, d, dev, 12, 12, "f64", False)
 
     if rank == 0:
         line = {

@@ -142,7 +142,7 @@ std::vector<View> source_views(const ModelData &d, const std::vector<int> &ev) {
 // Build the VE plans for a job: kind 0 = partition, kind 1 = marginals of targets.
 int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
                 int n_order, const std::vector<int> &targets, std::vector<VEPlan> &plans, int &max_width,
-                int64_t budget, int eb) {
+                int64_t budget, int eb, int part = 0, int n_parts = 1) {
     const int nv = (int)d.cards.size();
     auto scopes = conditioned_scopes(d, ev);
     auto views = source_views(d, ev);
@@ -193,16 +193,16 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                 if (ev[v] < 0) vars.push_back(v);
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
-        plans.push_back(plan_bucket_tree(d.cards, views, ord, targets));
+        plans.push_back(plan_bucket_tree(d.cards, views, ord, targets, part, n_parts));
         auto need = [&](const VEPlan &p) { return plan_peak_bytes(p, eb) + (int64_t)p.buckets.size() * 512; };
         const char *force = std::getenv("BNPP_TREE_SLOTS");     // testing / tuning: chain mode, fixed slots
         if (force && std::atoi(force) > 0) {
             std::string msg;
             VEPlan cp;
-            if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), cp, &msg))
+            if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), part, n_parts, cp, &msg))
                 return set_err(BNPP_ERR_UNSUPPORTED, msg);
             plans.back() = std::move(cp);
-        } else if (need(plans.back()) > budget) {
+        } else if (need(plans.back()) > budget || n_parts > 1) {
             // every forward message does not fit: recompute them from checkpoints
             // (chain-shaped trees), with as many checkpoint slots as fit
             std::string msg;
@@ -211,7 +211,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             while (lo <= hi) {
                 int mid = (lo + hi) / 2;
                 VEPlan cp;
-                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, cp, &msg)) break;
+                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, part, n_parts, cp, &msg)) break;
                 if (need(cp) <= budget) {
                     best_s = mid;
                     best = std::move(cp);
@@ -246,13 +246,13 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
 // arenas fit `budget` bytes; a batch runs as one level-aligned schedule.
 int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
                    int n_order, const std::vector<int> &targets, int dtype, int64_t budget,
-                   std::vector<Schedule> &out, double *stats) {
+                   std::vector<Schedule> &out, double *stats, int part = 0, int n_parts = 1) {
     std::vector<VEPlan> plans;
     int width = 0;
     const bool timing = std::getenv("BNPP_TIMING") != nullptr;
     double t0 = now_ms();
     const int eb = dtype == BNPP_F32 ? 4 : 8;
-    int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width, budget, eb);
+    int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width, budget, eb, part, n_parts);
     if (rc) return rc;
     if (timing) std::fprintf(stderr, "[bnpp] plans %.1f ms\n", now_ms() - t0);
     std::vector<int64_t> src_sizes;
@@ -314,7 +314,7 @@ int64_t memory_budget(bnpp_ctx *ctx) {
 
 int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals,
                int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
-               std::unique_ptr<bnpp_job> &job) {
+               std::unique_ptr<bnpp_job> &job, int part = 0, int n_parts = 1) {
     if (!ctx || !m) return set_err(BNPP_ERR_INVALID, "null context or model");
     if (dtype != BNPP_F32 && dtype != BNPP_F64) return set_err(BNPP_ERR_INVALID, "bad dtype");
     const ModelData &d = m->d;
@@ -335,8 +335,9 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
         }
     }
     std::vector<Schedule> batches;
+    if (n_parts < 1 || part < 0 || part >= n_parts) return set_err(BNPP_ERR_INVALID, "bad part / n_parts");
     int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, memory_budget(ctx),
-                            batches, job->stats);
+                            batches, job->stats, part, n_parts);
     if (rc) return rc;
     rc = upload_sources(ctx->c, d.values, dtype == BNPP_F32 ? kF32 : kF64, job->src);
     if (rc) return from_ctx(ctx, rc);
@@ -355,14 +356,17 @@ void destroy_job(bnpp_job *job) {
 
 // results of a launched job: partition -> out[0] = log10 Z (z_out: Z);
 // marginals -> sum(card) normalised values
-int job_results(bnpp_job *job, hipStream_t stream, double *out, double *z_out) {
+int job_results(bnpp_job *job, hipStream_t stream, double *out, double *z_out, int *owned = nullptr) {
     std::vector<std::vector<double>> vals;
     std::vector<int64_t> exp2;
     int rc = fetch_program(job->ctx->c, job->pg, stream, vals, exp2);
     if (rc) return from_ctx(job->ctx, rc);
     std::vector<const std::vector<int> *> rvars;
-    for (auto &ex : job->pg.parts)
+    std::vector<char> mine;
+    for (auto &ex : job->pg.parts) {
         for (auto &v : ex.sched.plan_result_vars) rvars.push_back(&v);
+        for (char c : ex.sched.plan_result_owned) mine.push_back(c);
+    }
     if (job->kind == 0) {
         double p = 0;                                   // part.partition(): sequential sum
         for (double v : vals[0]) p += v;
@@ -375,7 +379,11 @@ int job_results(bnpp_job *job, hipStream_t stream, double *out, double *z_out) {
         int t = job->targets[i];
         int k = job->cards[t];
         const std::vector<double> &r = vals[i];
-        if (job->ev_val[t] >= 0) {                      // evidence variable: one-hot
+        const bool own = i >= mine.size() || mine[i];
+        if (owned) owned[i] = own ? 1 : 0;
+        if (!own) {                                     // another part computes it
+            for (int s = 0; s < k; ++s) out[o + s] = 0.0;
+        } else if (job->ev_val[t] >= 0) {               // evidence variable: one-hot
             for (int s = 0; s < k; ++s) out[o + s] = s == job->ev_val[t] ? 1.0 : 0.0;
         } else if ((int)r.size() == k && k > 0 && rvars[i]->size() == 1) {
             double part = 0;                            // Factor::normalize (factor.cpp:244-255)
@@ -757,6 +765,29 @@ int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars,
     BNPP_GUARD_END
 }
 
+int bnpp_plan_tree_part(const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
+                        const int *order, int n_order, int part, int n_parts, int dtype, int *owned, double *stats,
+                        int n_stats) {
+    BNPP_GUARD_BEGIN
+    if (!m || !owned) return set_err(BNPP_ERR_INVALID, "null argument");
+    if (n_parts < 1 || part < 0 || part >= n_parts) return set_err(BNPP_ERR_INVALID, "bad part / n_parts");
+    std::vector<int> ev, targets;
+    std::string msg;
+    if (!evidence_array(m->d, n_ev, ev_vars, ev_vals, ev, msg)) return set_err(BNPP_ERR_INVALID, msg);
+    for (int v = 0; v < (int)m->d.cards.size(); ++v) targets.push_back(v);
+    std::vector<Schedule> batches;
+    double st[8] = {0};
+    int rc = plan_schedules(m->d, ev, 3, heuristic, order, n_order, targets, dtype, memory_budget(nullptr), batches, st,
+                            part, n_parts);
+    if (rc) return rc;
+    size_t i = 0;
+    for (auto &s : batches)
+        for (char c : s.plan_result_owned) owned[i++] = c ? 1 : 0;
+    for (int k = 0; stats && k < n_stats && k < 8; ++k) stats[k] = st[k];
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
 int bnpp_job_stats(const bnpp_job *job, double *stats, int n_stats) {
     if (!job || !stats) return set_err(BNPP_ERR_INVALID, "null argument");
     for (int i = 0; i < n_stats && i < 8; ++i) stats[i] = job->stats[i];
@@ -822,13 +853,21 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
 int bnpp_marginals_tree(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
                         int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
                         double *out, double *uptime_ms) {
+    return bnpp_marginals_tree_part(ctx, m, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, 0,
+                                    1, dtype, out, nullptr, uptime_ms);
+}
+
+int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                             int heuristic, const int *order, int n_order, int n_targets, const int *targets,
+                             int part, int n_parts, int dtype, double *out, int *owned, double *uptime_ms) {
     BNPP_GUARD_BEGIN
     if (!out) return set_err(BNPP_ERR_INVALID, "null output");
     double t0 = now_ms();
     std::unique_ptr<bnpp_job> job;
-    int rc = create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job);
+    int rc = create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job,
+                        part, n_parts);
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
-    if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
+    if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr, owned);
     if (job) destroy_job(job.release());
     if (rc) return rc;
     if (uptime_ms) *uptime_ms = now_ms() - t0;

@@ -515,7 +515,7 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
 }
 
 VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &sources,
-                        const std::vector<int> &order, const std::vector<int> &targets) {
+                        const std::vector<int> &order, const std::vector<int> &targets, int part, int n_parts) {
     VEPlan p;
     PlanBuilder B(cards, p, sources, order, true);
     const int nord = (int)order.size();
@@ -569,9 +569,12 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
     }
     // marginals: the belief of the target's bucket, or of the smallest
     // separator below it (lam_c * pi_c), summed down to the target
-    for (int t : targets) {
+    for (size_t ti = 0; ti < targets.size(); ++ti) {
+        const int t = targets[ti];
+        const bool mine = (int)(ti % (size_t)n_parts) == part;
+        p.results_owned.push_back(mine);
         int i = t >= 0 && t < (int)cards.size() ? B.rank[t] : -1;
-        if (i < 0 || lam[i] < 0) {                       // evidence / not eliminated / in no factor
+        if (!mine || i < 0 || lam[i] < 0) {              // other part / evidence / in no factor
             p.results.push_back(-1);
             p.results_vars.push_back({});
             continue;
@@ -612,7 +615,11 @@ int64_t binom_capped(int n, int k) {             // C(n, k), saturating at 2^40
 
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
-                            VEPlan &out, std::string *msg) {
+                            int part, int n_parts, VEPlan &out, std::string *msg) {
+    if (n_parts < 1 || part < 0 || part >= n_parts) {
+        if (msg) *msg = "bad part";
+        return false;
+    }
     VEPlan p;
     PlanBuilder B(cards, p, sources, order, true);
     B.sequential = true;
@@ -650,57 +657,77 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         return B.view(B.emit(in, order[i], false));
     };
     auto reduce_to = [&](std::vector<View> in, int t) { return B.reduce_to(std::move(in), t); };
+    // paths (leaf ... root); marginals are owned by contiguous segments of the
+    // concatenated paths, one segment per part
+    std::vector<std::vector<int>> paths;
     for (int top = 0; top < nord; ++top) {
         if (!has[top] || parent[top] >= 0) continue;
-        std::vector<int> path;                       // leaf ... root (child -> parent)
+        std::vector<int> path;
         for (int b = top; b >= 0; b = child[b]) path.push_back(b);
         std::reverse(path.begin(), path.end());
+        paths.push_back(path);
+    }
+    int64_t total = 0;
+    for (auto &pa : paths) total += (int64_t)pa.size();
+    const int64_t g_lo = total * part / n_parts, g_hi = total * (part + 1) / n_parts;
+    std::vector<char> owned_var(cards.size(), part == 0 ? 1 : 0);   // variables on no path: part 0
+    int64_t off = 0;
+    for (const std::vector<int> &path : paths) {
         const int m = (int)path.size();
+        for (int q = 0; q < m; ++q) owned_var[order[path[q]]] = 0;
+        const int a = (int)std::max<int64_t>(0, std::min<int64_t>(m, g_lo - off));
+        const int b = (int)std::max<int64_t>(0, std::min<int64_t>(m, g_hi - off));
+        off += m;
+        if (a >= b) continue;
+        for (int q = a; q < b; ++q) owned_var[order[path[q]]] = 1;
         // backward sweep state: pi of path[j] (message from path[j+1] into path[j])
         View pi_cur;
         bool have_pi = false;                        // pi of the root: constant 1
-        int next_deliver = m - 2;
-        // deliver(j): lam_j is live.  pi_j = sum F_{j+1} * pi_{j+1} down to sep_j;
-        // marginal of x_{j+1} = lam_j * pi_j summed down to x_{j+1}
-        auto deliver = [&](int j, const View &lam_j) {
-            if (j != next_deliver) return false;
+        // pi_j = sum F_{j+1} * pi_{j+1} down to sep_j (needs no forward message)
+        auto pi_step = [&](int j, const std::vector<int> &sep_j) {
             const int q = path[j + 1];
             std::vector<View> in = src_in[q];
             if (have_pi) in.push_back(pi_cur);
-            View pij;
-            bool hp = false;
-            if (!in.empty()) {
-                std::vector<int> y;
-                for (int v : chain_scope(in))
-                    if (std::find(lam_j.vars.begin(), lam_j.vars.end(), v) == lam_j.vars.end()) y.push_back(v);
-                std::sort(y.begin(), y.end(), [&](int a, int b) { return B.rank[a] < B.rank[b]; });
-                if (y.empty() && in.size() == 1) {
-                    pij = in[0];
-                } else {
-                    int tb = B.emit(in, y.empty() ? -1 : y[0], false);
-                    for (size_t k = 1; k < y.size(); ++k) tb = B.emit({B.view(tb)}, y[k], false);
-                    pij = B.view(tb);
-                }
-                hp = true;
+            if (in.empty()) {
+                have_pi = false;
+                return;
             }
+            std::vector<int> y;
+            for (int v : chain_scope(in))
+                if (std::find(sep_j.begin(), sep_j.end(), v) == sep_j.end()) y.push_back(v);
+            std::sort(y.begin(), y.end(), [&](int u, int w) { return B.rank[u] < B.rank[w]; });
+            if (y.empty() && in.size() == 1) {
+                pi_cur = in[0];
+            } else {
+                int tb = B.emit(in, y.empty() ? -1 : y[0], false);
+                for (size_t k = 1; k < y.size(); ++k) tb = B.emit({B.view(tb)}, y[k], false);
+                pi_cur = B.view(tb);
+            }
+            have_pi = true;
+        };
+        // deliveries j in [lo, hi): marginal of x_{j+1} = lam_j * pi_j summed down to it
+        const int lo = std::max(a - 1, 0), hi = b - 1;
+        for (int j = m - 2; j >= std::max(hi, 0); --j) pi_step(j, lam_vars[path[j]]);   // suffix: pi only
+        int next_deliver = hi - 1;
+        auto deliver = [&](int j, const View &lam_j) {
+            if (j != next_deliver) return false;
+            pi_step(j, lam_j.vars);
             std::vector<View> bel{lam_j};
-            if (hp) bel.push_back(pij);
-            result_of[order[q]] = reduce_to(bel, order[q]);
-            pi_cur = pij;
-            have_pi = hp;
+            if (have_pi) bel.push_back(pi_cur);
+            result_of[order[path[j + 1]]] = reduce_to(bel, order[path[j + 1]]);
             --next_deliver;
             return true;
         };
         // reverse(lo, hi, start, s): deliver j = hi-1 ... lo; `start` = lam_{lo-1}
         // (null for lo == 0), s free checkpoint slots (binomial checkpointing)
         bool ok = true;
-        std::function<void(int, int, const View *, int)> reverse = [&](int lo, int hi, const View *start, int sl) {
-            const int len = hi - lo;
+        std::function<void(int, int, const View *, int)> reverse = [&](int rlo, int rhi, const View *start, int sl) {
+            const int len = rhi - rlo;
             if (len <= 0 || !ok) return;
             if (len == 1 || sl <= 0) {
-                for (int j = hi - 1; j >= lo; --j) {          // stream lam_lo..lam_j, deliver lam_j
-                    View cur = forward(path[lo], start);
-                    for (int k = lo + 1; k <= j; ++k) cur = forward(path[k], &cur);
+                for (int j = rhi - 1; j >= rlo; --j) {        // stream lam_rlo..lam_j, deliver lam_j
+                    View cur = forward(path[rlo], start);
+                    for (int k = rlo + 1; k <= j; ++k) cur = forward(path[k], &cur);
                     ok = ok && deliver(j, cur);
                 }
                 return;
@@ -709,27 +736,34 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             while (binom_capped(sl + r, sl) < len) ++r;
             int64_t right_cap = binom_capped(sl - 1 + r, sl - 1);
             int d = (int)std::max<int64_t>(1, len - std::min<int64_t>(right_cap, len - 1));
-            View ck = forward(path[lo], start);                // advance d steps, keep lam_{lo+d-1}
-            for (int k = lo + 1; k < lo + d; ++k) ck = forward(path[k], &ck);
-            const int c = lo + d - 1;
-            reverse(c + 1, hi, &ck, sl - 1);
+            View ck = forward(path[rlo], start);               // advance d steps, keep lam_{rlo+d-1}
+            for (int k = rlo + 1; k < rlo + d; ++k) ck = forward(path[k], &ck);
+            const int c = rlo + d - 1;
+            reverse(c + 1, rhi, &ck, sl - 1);
             ok = ok && deliver(c, ck);
-            reverse(lo, c, start, sl);
+            reverse(rlo, c, start, sl);
         };
-        reverse(0, m - 1, nullptr, slots);
-        if (!ok || next_deliver != -1) {
+        if (hi > lo) {
+            View start;                                        // prefix: stream lam_0 .. lam_{lo-1}
+            for (int k = 0; k < lo; ++k) start = forward(path[k], k ? &start : nullptr);
+            reverse(lo, hi, lo ? &start : nullptr, slots);
+        }
+        if (!ok || next_deliver != lo - 1) {
             if (msg) *msg = "internal: checkpoint schedule out of order";
             return false;
         }
-        // the leaf's marginal: its own bucket with the message from above
-        std::vector<View> bel = src_in[path[0]];
-        if (have_pi) bel.push_back(pi_cur);
-        result_of[order[path[0]]] = reduce_to(bel, order[path[0]]);
+        if (a == 0) {                                          // the leaf: its own bucket and pi_0
+            std::vector<View> bel = src_in[path[0]];
+            if (have_pi) bel.push_back(pi_cur);
+            result_of[order[path[0]]] = reduce_to(bel, order[path[0]]);
+        }
     }
     for (int t : targets) {
-        int r = t >= 0 && t < (int)cards.size() ? result_of[t] : -1;
+        bool in_range = t >= 0 && t < (int)cards.size();
+        int r = in_range ? result_of[t] : -1;
         p.results.push_back(r);
         p.results_vars.push_back(r >= 0 ? p.msgs[r - p.n_src].vars : std::vector<int>{});
+        p.results_owned.push_back(in_range ? owned_var[t] : (part == 0));
     }
     B.finish();
     out = std::move(p);
@@ -854,6 +888,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
             if (res[r] >= 0) last[remap(pi, res[r])] = kForever;
             s.plan_result_table.push_back(res[r] >= 0 ? remap(pi, res[r]) : -1);
             s.plan_result_vars.push_back(res_vars[r]);
+            s.plan_result_owned.push_back(r < plans[pi]->results_owned.size() ? plans[pi]->results_owned[r] : 1);
         }
     }
     std::vector<std::vector<int>> born_at(n_levels + 2), dies_at(n_levels + 2);

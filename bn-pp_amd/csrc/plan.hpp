@@ -66,6 +66,7 @@ struct VEPlan {
     // no table (evidence / variable in no factor); replaces result_table
     std::vector<int> results;
     std::vector<std::vector<int>> results_vars;
+    std::vector<char> results_owned;    // per result: computed by this part (empty: all)
     // cards of the model followed by virtual (composite) variables the plan
     // sums in one pass; empty: the model's cards
     std::vector<int> cards_ext;
@@ -90,17 +91,23 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
 // message and its other children's messages, summed down to the child's
 // separator; each target's marginal (unnormalised) is the smallest belief that
 // contains it summed down to the target.  results[i] -> targets[i].
+// part / n_parts: marginals of targets i with i % n_parts == part only (the
+// forward and backward passes are computed in full by every part).
 VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &sources,
-                        const std::vector<int> &order, const std::vector<int> &targets);
+                        const std::vector<int> &order, const std::vector<int> &targets, int part = 0,
+                        int n_parts = 1);
 
 // The same marginals in bounded memory when the bucket tree is a chain (a
 // column-sweep order on a grid): forward messages are recomputed from `slots`
 // checkpoints by binomial checkpointing (revolve), buckets run in program order
 // (one level each) so the arena holds about slots + 5 messages.  Returns false
-// (msg) when the tree is not a chain.
+// (msg) when the tree is not a chain.  part / n_parts: this part owns the
+// marginals of one contiguous segment of the chain; it streams the forward
+// messages up to the segment, runs the backward messages (which need no
+// forward message) down to it, and checkpoints only inside it.
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
-                            VEPlan &out, std::string *msg);
+                            int part, int n_parts, VEPlan &out, std::string *msg);
 
 // Flattened, level-ordered launch schedule over one or more plans sharing the
 // same sources.  Tables: [0, n_src) sources, then every plan's messages.
@@ -120,6 +127,7 @@ struct Schedule {
     int n_levels = 0;
     std::vector<int> plan_result_table;     // per plan (-1: constant 1)
     std::vector<std::vector<int>> plan_result_vars;
+    std::vector<char> plan_result_owned;     // per result: 0 = another part computes it
     int64_t arena_bytes = 0;
     double entries = 0;
     double elems_moved = 0;

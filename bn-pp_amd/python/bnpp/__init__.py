@@ -65,6 +65,8 @@ _SIGS = {
     "bnpp_partition": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _DP, _DP, _DP]),
     "bnpp_marginals": (_I, [_P, _P, _I, _IP, _IP, _I, _I, _IP, _I, _DP, _DP]),
     "bnpp_marginals_tree": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, _DP, _DP]),
+    "bnpp_marginals_tree_part": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, _I, _I, _DP, _IP, _DP]),
+    "bnpp_plan_tree_part": (_I, [_P, _I, _IP, _IP, _I, _IP, _I, _I, _I, _I, _IP, _DP, _I]),
     "bnpp_variable_elimination": (_I, [_P, _P, _I, _IP, _I, _I, _I, _IP, _IP, C.c_int64, C.POINTER(C.c_int64), _DP,
                                        C.POINTER(C.c_int64)]),
     "bnpp_plan_stats": (_I, [_P, _I, _I, _IP, _IP, _I, _IP, _I, _I, _DP, _I]),
@@ -268,24 +270,42 @@ def marginals(ctx: Context, model: Model, evidence=None, heuristic: str = "mf", 
 
 
 def marginals_tree(ctx: Context, model: Model, evidence=None, heuristic: str = "mf", dtype: int = F64,
-                   targets: Optional[Sequence[int]] = None, order: Optional[Sequence[int]] = None):
+                   targets: Optional[Sequence[int]] = None, order: Optional[Sequence[int]] = None,
+                   part: int = 0, n_parts: int = 1):
     """All marginals from one two-pass bucket tree (bnpp_marginals_tree) ->
-    ({var: [p_0..p_k-1]}, uptime_ms).  Same output as marginals(), to rounding."""
+    ({var: [p_0..p_k-1]}, uptime_ms).  Same output as marginals(), to rounding.
+    part / n_parts (bnpp_marginals_tree_part): only the targets this part owns."""
     n, ev_v, ev_x = _ev(evidence)
     tg = list(range(model.n_vars)) if targets is None else list(targets)
     total = sum(model.cards[t] for t in tg)
     out = (C.c_double * max(total, 1))()
+    owned = (C.c_int * max(len(tg), 1))()
     up = C.c_double()
     oa = _ints(list(order)) if order is not None else None
     h = ORDER_GIVEN if order is not None else HEURISTICS[heuristic]
-    _check(_lib.bnpp_marginals_tree(ctx.handle, model.handle, n, ev_v, ev_x, h, oa,
-                                    len(order) if order is not None else 0, len(tg), _ints(tg), dtype, out,
-                                    C.byref(up)), "bnpp_marginals_tree")
+    _check(_lib.bnpp_marginals_tree_part(ctx.handle, model.handle, n, ev_v, ev_x, h, oa,
+                                         len(order) if order is not None else 0, len(tg), _ints(tg), part, n_parts,
+                                         dtype, out, owned, C.byref(up)), "bnpp_marginals_tree_part")
     res, o = {}, 0
-    for t in tg:
-        res[t] = list(out[o:o + model.cards[t]])
+    for i, t in enumerate(tg):
+        if owned[i]:
+            res[t] = list(out[o:o + model.cards[t]])
         o += model.cards[t]
     return res, up.value
+
+
+def plan_tree_part(model: Model, part: int, n_parts: int, evidence=None, heuristic: str = "mf", dtype: int = F64,
+                   order: Optional[Sequence[int]] = None):
+    """Host-only plan of one part of the bucket-tree marginals ->
+    (owned variable ids, stats list as Job)."""
+    n, ev_v, ev_x = _ev(evidence)
+    owned = (C.c_int * max(model.n_vars, 1))()
+    st = (C.c_double * 8)()
+    oa = _ints(list(order)) if order is not None else None
+    h = ORDER_GIVEN if order is not None else HEURISTICS[heuristic]
+    _check(_lib.bnpp_plan_tree_part(model.handle, n, ev_v, ev_x, h, oa, len(order) if order is not None else 0,
+                                    part, n_parts, dtype, owned, st, 8), "bnpp_plan_tree_part")
+    return [v for v in range(model.n_vars) if owned[v]], list(st)
 
 
 def variable_elimination(ctx: Context, model: Model, variables: Sequence[int], heuristic: str = "given",

@@ -37,26 +37,46 @@ def log10_sum(logs: Sequence[float]) -> float:
     return m + math.log10(sum(10.0 ** (x - m) for x in finite))
 
 
-def sharded_marginals(n_vars: int, cards: Sequence[int], rank: int, world: int,
-                      compute: Callable[[List[int]], Dict[int, List[float]]], dist=None) -> Dict[int, List[float]]:
-    """All marginals, each rank computing its round-robin share of targets;
-    assembled by one all_reduce(SUM) over a flat float64 vector."""
+def assemble_marginals(n_vars: int, cards: Sequence[int], part: Dict[int, List[float]],
+                       dist=None) -> Dict[int, List[float]]:
+    """Every rank contributes the marginals it owns (the others read as zero);
+    one all_reduce(SUM) of a sum(card)-long fp64 vector assembles them all."""
     import torch
 
-    mine = shard(list(range(n_vars)), rank, world)
-    part = compute(mine) if mine else {}
     offs = [0]
     for c in cards:
         offs.append(offs[-1] + c)
     flat = torch.zeros(offs[-1], dtype=torch.float64)
     for t, vals in part.items():
         flat[offs[t]:offs[t] + cards[t]] = torch.tensor(vals, dtype=torch.float64)
-    if dist is not None and world > 1:
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
         dev = _comm_device(dist)
         buf = flat.to(dev)
         dist.all_reduce(buf, op=dist.ReduceOp.SUM)
         flat = buf.cpu()
     return {t: flat[offs[t]:offs[t + 1]].tolist() for t in range(n_vars)}
+
+
+def sharded_tree_marginals(ctx, model, rank: int, world: int, dist=None, evidence=None, heuristic: str = "mf",
+                           dtype=None, order=None) -> Dict[int, List[float]]:
+    """Bucket-tree marginals on `world` GPUs: part `rank` of
+    bnpp_marginals_tree_part (a contiguous segment of a chain-shaped tree: its
+    forward prefix, the backward messages down to it, checkpointed recomputation
+    inside it), then one all_reduce(SUM)."""
+    import bnpp
+
+    mine, _ = bnpp.marginals_tree(ctx, model, evidence, heuristic, bnpp.F64 if dtype is None else dtype,
+                                  order=order, part=rank, n_parts=world)
+    return assemble_marginals(model.n_vars, model.cards, mine, dist)
+
+
+def sharded_marginals(n_vars: int, cards: Sequence[int], rank: int, world: int,
+                      compute: Callable[[List[int]], Dict[int, List[float]]], dist=None) -> Dict[int, List[float]]:
+    """All marginals, each rank computing its round-robin share of targets;
+    assembled by one all_reduce(SUM) over a flat float64 vector."""
+    mine = shard(list(range(n_vars)), rank, world)
+    part = compute(mine) if mine else {}
+    return assemble_marginals(n_vars, cards, part, dist if world > 1 else None)
 
 
 def cutset_assignments(cut_vars: Sequence[int], cards: Sequence[int]) -> List[Dict[int, int]]:

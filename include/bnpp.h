@@ -157,6 +157,16 @@ int bnpp_marginals_tree(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int 
                         int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
                         double *out, double *uptime_ms);
 
+/* One part of bnpp_marginals_tree for multi-GPU runs (one process per GPU,
+ * part = rank, n_parts = world size): this part computes only the marginals it
+ * owns (a contiguous segment of a chain-shaped bucket tree, else every
+ * n_parts-th target) and writes zeros for the others; owned[i] (optional)
+ * flags targets[i].  Summing `out` over the parts gives bnpp_marginals_tree's
+ * output (one all-reduce, no other exchange). */
+int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                             int heuristic, const int *order, int n_order, int n_targets, const int *targets,
+                             int part, int n_parts, int dtype, double *out, int *owned, double *uptime_ms);
+
 /* BN::variable_elimination (model.cpp:348-446) over the factors of `m` taken
  * as given (already conditioned by the caller): eliminates `vars` (heuristic
  * order, or exactly this order with BNPP_ORDER_GIVEN) and returns the result
@@ -172,6 +182,14 @@ int bnpp_variable_elimination(bnpp_ctx *ctx, const bnpp_model *m, int n_vars, co
  * bnpp_job_stats. */
 int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
                     const int *order, int n_order, int dtype, double *stats, int n_stats);
+
+/* Host-only planning of one part of bnpp_marginals_tree_part (all variables
+ * as targets): owned[v] = 1 when this part computes v's marginal; stats as
+ * bnpp_job_stats for this part's plan (may be NULL).  The memory budget is
+ * BNPP_MEM_BUDGET_GB or 64 GB (no device is consulted). */
+int bnpp_plan_tree_part(const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
+                        const int *order, int n_order, int part, int n_parts, int dtype, int *owned, double *stats,
+                        int n_stats);
 
 /* ------------------------------------------- prepared jobs (benchmark) */
 /* A planned, device-resident inference that can be launched repeatedly. */

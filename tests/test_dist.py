@@ -89,3 +89,49 @@ def test_shard_and_logsum_helpers():
     assert bdist.log10_sum([-math.inf]) == -math.inf
     a = bdist.cutset_assignments([1, 4], [2, 3, 2, 2, 3])
     assert len(a) == 9 and a[0] == {1: 0, 4: 0}
+
+
+def _tree_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(REPO, "bn-pp_amd", "python"))
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import torch.distributed as dist
+    import bnpp
+    import refcpu
+    from bnpp import dist as bdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    path = model_path("ising8x8.uai")
+    m = bnpp.Model.load(path)
+    col = [r * 8 + c for c in range(8) for r in range(8)]
+    owned, _ = bnpp.plan_tree_part(m, rank, world, {}, order=col)   # the engine's ownership rule
+    rm = refcpu.Model.load(path)
+    mine = {t: rm.marginal(t, {}, "mf") for t in owned}            # oracle as the per-rank compute
+    q.put((rank, bdist.assemble_marginals(m.n_vars, m.cards, mine, dist), owned))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tree_part_assembly_world2():
+    """Chain-segment ownership of bnpp_marginals_tree_part + one all_reduce
+    assemble every marginal exactly once (gloo, world size 2)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import refcpu
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full, _ = refcpu.Model.load(model_path("ising8x8.uai")).marginals({}, "mf")
+    owned = sorted(sum([r[2] for r in res], []))
+    assert owned == list(range(64))
+    for rank, marg, _ in res:
+        for t in range(64):
+            assert marg[t] == pytest.approx(full[t], abs=1e-12), (rank, t)

@@ -155,3 +155,21 @@ def test_tree_chain_mode_rejects_non_chain(ctx):
         assert e.value.status == bnpp.ERR_UNSUPPORTED
     finally:
         del os.environ["BNPP_TREE_SLOTS"]
+
+
+@pytest.mark.parametrize("n_parts", [2, 3, 5])
+def test_tree_parts_sum_to_whole(ctx, n_parts):
+    """bnpp_marginals_tree_part: each part's owned marginals equal the whole
+    tree's, and the parts cover every target once (chain segments with the
+    forward prefix streamed and the backward messages run down to the segment)."""
+    m = bnpp.Model.from_dict(synth.ising_grid(7, 11, seed=12))
+    col = [r * 11 + c for c in range(11) for r in range(7)]
+    ev = {20: 0}
+    want, _ = bnpp.marginals(ctx, m, ev, "mf", bnpp.F64)
+    seen = []
+    for part in range(n_parts):
+        got, _ = bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F64, order=col, part=part, n_parts=n_parts)
+        seen += list(got)
+        for t, p in got.items():
+            assert _close(p, want[t], 1e-12), (part, t, p, want[t])
+    assert sorted(seen) == list(range(m.n_vars))

@@ -171,3 +171,26 @@ def test_plan_stats_checkpointed_chain():
     assert ck[0] > full[0]                           # recomputation
     assert ck[2] == ck[3]                            # one bucket per level
     assert ck[1] < full[1]                           # smaller arena
+
+
+@pytest.mark.parametrize("n_parts", [1, 2, 3, 8])
+def test_tree_parts_cover_every_marginal_once(n_parts):
+    """bnpp_marginals_tree_part's ownership: every variable exactly once over
+    the parts, contiguous segments of the chain for a column-sweep order, and
+    per-part work well below a whole tree when the chain is split."""
+    m = bnpp.Model.load(model_path("ising10x10.uai"))
+    col = [r * 10 + c for c in range(10) for r in range(10)]
+    seen = []
+    for part in range(n_parts):
+        owned, st = bnpp.plan_tree_part(m, part, n_parts, {}, order=col)
+        pos = sorted(col.index(v) for v in owned)
+        assert pos == list(range(pos[0], pos[0] + len(pos))) if pos else True
+        seen += owned
+    assert sorted(seen) == list(range(m.n_vars))
+    # a non-chain tree (min-fill on alarm with evidence) is dealt round robin
+    a = bnpp.Model.load(model_path("alarm.uai"))
+    ev = bnpp.load_evidence(model_path("alarm.uai.evid"))
+    seen = []
+    for part in range(n_parts):
+        seen += bnpp.plan_tree_part(a, part, n_parts, ev)[0]
+    assert sorted(seen) == list(range(a.n_vars))
