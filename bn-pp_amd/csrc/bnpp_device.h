@@ -36,6 +36,8 @@ struct TableMeta {
 enum BucketFlags : int32_t {
     kScale = 1,        // renormalise by the inputs' max exponents (exact power-of-two)
     kTrackMax = 2,     // raise meta[out].maxbits
+    kOutStrided = 4,   // dims permuted: output offset from per-dim output strides
+                       // (n_dims words after the dims rows in the pool)
 };
 
 // Each thread evaluates a V1 x V2 register tile of the output: V1 entries of
@@ -81,8 +83,8 @@ constexpr int kStreamLdsBudget = 32768;    // bytes of LDS for the small inputs
 // launch gets the register allocation of its own shape.
 __host__ __device__ inline int nin_class(int n_in) { return n_in <= 1 ? 1 : n_in <= 2 ? 2 : n_in <= 4 ? 4 : 8; }
 __host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return nin_class(n_in) * 64 + v1 * 8 + v2; }
-// stream kernels: 4096 + big-class * 64 + v1 * 8 + v2
-__host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 64 + v1 * 8 + v2; }
+// stream kernels: 4096 + big-class * 256 + v1 * 16 + v2  (v1, v2 <= 8)
+__host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 256 + v1 * 16 + v2; }
 
 // dims pool, per output dim (fastest first): 2 + n_in int64 words
 //   w0 = card | (shift << 32) | (pow2 << 40)    w1 = magic    w2.. = stride per input

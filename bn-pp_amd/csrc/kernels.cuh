@@ -472,26 +472,31 @@ struct StreamState {
 
 template <typename T, int V1, int V2, int BC>
 __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const StreamState &st, const T *small,
-                                                 int64_t tid, T (&acc)[V1 * V2]) {
+                                                 int64_t tid, T (&acc)[V1 * V2], int64_t &out_off) {
+    constexpr bool kRows = (BC == kBigInter2 || BC == kBigInter4) && V2 > 1;   // output rows at a stride
     constexpr int TS = V1 * V2;
     using BT = BigTile<T, V1, V2, BC>;
     int64_t pos[kStreamMaxIn];
 #pragma unroll
     for (int i = 0; i < kStreamMaxIn; ++i) pos[i] = b.base[i];
+    out_off = 0;
     if (b.n_dims > 0) {
+        const int row = 2 + b.n_in;
+        const int64_t *os = b.dims + (int64_t)b.n_dims * row;   // kOutStrided: output stride per dim
         uint64_t q, r;
         divmod_dim((uint64_t)tid, b.t0h, b.t0m, q, r);
         int64_t i0 = (int64_t)r * V1;
 #pragma unroll
         for (int i = 0; i < kStreamMaxIn; ++i) pos[i] += i0 * b.s0[i];
+        if constexpr (kRows) out_off = i0 * os[0];
         if (b.n_dims > 1) {
             uint64_t q1, r1;
             divmod_dim(q, b.t1h, b.t1m, q1, r1);
             int64_t i1 = (int64_t)r1 * V2;
 #pragma unroll
             for (int i = 0; i < kStreamMaxIn; ++i) pos[i] += i1 * b.s1[i];
+            if constexpr (kRows) out_off += i1 * os[1];
             uint64_t rem = q1;
-            const int row = 2 + b.n_in;
             const int64_t *dp = b.dims + 2 * row;
             for (int j = 2; j < b.n_dims; ++j) {
                 uint64_t qq, rr;
@@ -499,6 +504,7 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
 #pragma unroll
                 for (int i = 0; i < kStreamMaxIn; ++i)
                     if (i < b.n_in) pos[i] += (int64_t)rr * dp[2 + i];
+                if constexpr (kRows) out_off += (int64_t)rr * os[j];
                 rem = qq;
                 dp += row;
             }
@@ -571,9 +577,9 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
             T p[TS];
 #pragma unroll
             for (int j = 0; j < TS; ++j) p[j] = T(1);
-            smalls(v, p, [&](T (&q)[TS]) {
+            smalls(v, p, [&](T (&q)[TS]) {                 // same big values for every row j / V1
 #pragma unroll
-                for (int j = 0; j < TS; ++j) q[j] = q[j] * all[j * K + v];
+                for (int j = 0; j < TS; ++j) q[j] = q[j] * all[(j % V1) * K + v];
             });
 #pragma unroll
             for (int j = 0; j < TS; ++j) acc[j] = acc[j] + p[j];
@@ -639,6 +645,24 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
 #pragma unroll
     for (int j = 0; j < TS; ++j) m = acc[j] > m ? acc[j] : m;
     return m;
+}
+
+// store one stream tile: V2 rows of V1 entries at the output stride of dim 1
+// (interleaved tiles over a broadcast dim), else the contiguous-tile path
+template <typename T, int V1, int V2, int BC>
+__device__ __forceinline__ void stream_store(const LoadedBucket &b, int64_t tid0, int64_t tid, int64_t out_off,
+                                             const T (&acc)[V1 * V2], unsigned char *stage) {
+    if constexpr ((BC == kBigInter2 || BC == kBigInter4) && V2 > 1) {
+        if (tid < b.n_tiles) {
+            const int64_t os1 = b.dims[(int64_t)b.n_dims * (2 + b.n_in) + 1];
+            T *o = static_cast<T *>(b.out) + out_off;
+#pragma unroll
+            for (int j2 = 0; j2 < V2; ++j2) store_n<T, V1, kNtStore>(o + j2 * os1, acc + j2 * V1);
+        }
+    } else {
+        store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
+                                stage + (threadIdx.x >> 6) * kLdsWaveBytes);
+    }
 }
 
 // copy every small input of the bucket into LDS (uniform control flow)
@@ -716,12 +740,12 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_level_ker
         const int64_t tid0 = (vb - cur_begin) * kBlock;
         const int64_t tid = tid0 + threadIdx.x;
         T acc[V1 * V2];
+        int64_t oo = 0;
         if (tid < b.n_tiles) {
-            T m = compute_stream_tile<T, V1, V2, BC>(b, st, small, tid, acc);
+            T m = compute_stream_tile<T, V1, V2, BC>(b, st, small, tid, acc, oo);
             lmax = m > lmax ? m : lmax;
         }
-        store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
-                                stage + (threadIdx.x >> 6) * kLdsWaveBytes);
+        stream_store<T, V1, V2, BC>(b, tid0, tid, oo, acc, stage);
     }
     if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
 }
@@ -750,9 +774,9 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_single_ke
     for (int64_t tid0 = (int64_t)blockIdx.x * kBlock; tid0 < b.n_tiles; tid0 += (int64_t)gridDim.x * kBlock) {
         const int64_t tid = tid0 + threadIdx.x;
         T acc[V1 * V2];
-        if (tid < b.n_tiles) (void)compute_stream_tile<T, V1, V2, BC>(b, st, small, tid, acc);
-        store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
-                                stage + (threadIdx.x >> 6) * kLdsWaveBytes);
+        int64_t oo = 0;
+        if (tid < b.n_tiles) (void)compute_stream_tile<T, V1, V2, BC>(b, st, small, tid, acc, oo);
+        stream_store<T, V1, V2, BC>(b, tid0, tid, oo, acc, stage);
     }
 }
 
@@ -793,16 +817,18 @@ static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_
 }
 
 #define BNPP_STREAM_BC(X, T, V1, V2) X(T, V1, V2, 1) X(T, V1, V2, 2) X(T, V1, V2, 3) X(T, V1, V2, 4) X(T, V1, V2, 5)
-#define BNPP_STREAM_INTER(X, T) X(T, 2, 1, 6) X(T, 4, 1, 6) X(T, 2, 1, 7) X(T, 4, 1, 7)
+#define BNPP_STREAM_INTER(X, T) X(T, 2, 1, 6) X(T, 4, 1, 6) X(T, 8, 1, 6) X(T, 2, 1, 7) X(T, 4, 1, 7) X(T, 8, 1, 7) \
+    X(T, 4, 2, 6) X(T, 8, 2, 6) X(T, 4, 4, 6) X(T, 4, 2, 7) X(T, 8, 2, 7) X(T, 4, 4, 7) X(T, 2, 2, 6) X(T, 2, 2, 7) \
+    X(T, 2, 4, 6) X(T, 2, 4, 7)
 #define BNPP_STREAM_F32(X, T) BNPP_STREAM_INTER(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
     BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2) BNPP_STREAM_BC(X, T, 4, 4) \
     BNPP_STREAM_BC(X, T, 2, 8)
 #define BNPP_STREAM_F64(X, T) BNPP_STREAM_INTER(X, T) BNPP_STREAM_BC(X, T, 1, 1) BNPP_STREAM_BC(X, T, 2, 1) BNPP_STREAM_BC(X, T, 4, 1) \
     BNPP_STREAM_BC(X, T, 2, 2) BNPP_STREAM_BC(X, T, 2, 4) BNPP_STREAM_BC(X, T, 4, 2)
 #define BNPP_CASE_SLEVEL(T, V1, V2, BC) \
-    case 4096 + BC * 64 + V1 * 8 + V2: return go_stream_level<T, V1, V2, BC>(a, small_elems, max_grid, stream);
+    case 4096 + BC * 256 + V1 * 16 + V2: return go_stream_level<T, V1, V2, BC>(a, small_elems, max_grid, stream);
 #define BNPP_CASE_SSINGLE(T, V1, V2, BC) \
-    case 4096 + BC * 64 + V1 * 8 + V2: return go_stream_single<T, V1, V2, BC>(a, max_grid, stream);
+    case 4096 + BC * 256 + V1 * 16 + V2: return go_stream_single<T, V1, V2, BC>(a, max_grid, stream);
 
 #define BNPP_TILES_F32(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
     X(T, NIN, 4, 2) X(T, NIN, 4, 4) X(T, NIN, 2, 8)

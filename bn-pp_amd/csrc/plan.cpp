@@ -168,6 +168,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         }
         if (!ok) merged.push_back(dm);
     }
+    std::vector<int64_t> out_strides;     // kOutStrided: output stride per (permuted) dim
     int k = 1;
     int64_t es[kMaxIn] = {0};
     if (b.elim_var >= 0) {
@@ -267,10 +268,61 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 inter = b.in[big].base % vw == 0 && (int64_t)(v1 * k) % vw == 0;
                 for (size_t j = 1; inter && j < merged.size(); ++j)
                     if (merged[j].s[big] % vw) inter = false;
-                if (inter && v2 > 1) {
+                // wider tiles keep more bytes in flight per thread: 8 entries of dim 0
+                const char *iv = std::getenv("BNPP_INTER_V1");
+                const int want_v1 = iv ? std::atoi(iv) : 8;
+                int nv1 = v1;
+                if (want_v1 == 8 && merged[0].card % 8 == 0 && (int64_t)(8 * k) % vw == 0) nv1 = 8;
+                // a dim the big input does not vary along (a variable only the small
+                // inputs hold): the tile spans it, so one load of the big values
+                // serves every row; it becomes dim 1 and the output offsets come
+                // from per-dim output strides (kOutStrided)
+                int bdim = -1;
+                for (size_t j = 1; inter && j < merged.size(); ++j)
+                    if (merged[j].s[big] == 0 && (merged[j].card == 2 || merged[j].card == 4)) {
+                        bdim = (int)j;
+                        break;
+                    }
+                const char *nb = std::getenv("BNPP_NO_BCAST_ROWS");
+                if (nb && *nb == '1') bdim = -1;
+                if (inter && bdim >= 1) {
+                    const int cb = (int)merged[bdim].card;
+                    const int max_ts = eb == 4 ? 16 : 8;
+                    int rv1 = nv1;
+                    while (rv1 * cb > max_ts) rv1 /= 2;
+                    if (rv1 >= 2 && merged[0].card % (uint64_t)rv1 == 0 && (int64_t)(rv1 * k) % vw == 0) {
+                        std::vector<int64_t> os(merged.size());
+                        int64_t acc_s = 1;
+                        for (size_t j = 0; j < merged.size(); ++j) {
+                            os[j] = acc_s;
+                            acc_s *= (int64_t)merged[j].card;
+                        }
+                        Dim mb = merged[bdim];
+                        int64_t ob = os[bdim];
+                        merged.erase(merged.begin() + bdim);
+                        os.erase(os.begin() + bdim);
+                        merged.insert(merged.begin() + 1, mb);
+                        os.insert(os.begin() + 1, ob);
+                        out_strides = os;
+                        v1 = rv1;
+                        v2 = cb;
+                        d.v1 = v1;
+                        d.v2 = v2;
+                        d.n_tiles = out_size / (v1 * v2);
+                        d.flags |= kOutStrided;
+                        divisor(merged[0].card / v1, d.tdiv0);
+                        divisor(1, d.tdiv1);
+                    } else {
+                        bdim = -1;
+                    }
+                }
+                if (inter && bdim < 1 && (v2 > 1 || nv1 != v1)) {
+                    v1 = nv1;
                     v2 = 1;
+                    d.v1 = v1;
                     d.v2 = 1;
                     d.n_tiles = out_size / v1;
+                    divisor(merged[0].card / v1, d.tdiv0);
                     divisor(merged.size() < 2 ? 1 : merged[1].card, d.tdiv1);
                 }
             }
@@ -301,6 +353,8 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         pool.push_back((int64_t)magic);
         for (int i = 0; i < n; ++i) pool.push_back(dm.s[i]);
     }
+    if (d.flags & kOutStrided)
+        for (int64_t o : out_strides) pool.push_back(o);
     return true;
 }
 

@@ -173,6 +173,39 @@ def test_interleaved_stream_buckets(ctx, k, n_other):
         assert max(abs(a - b) / abs(b) for a, b in zip(vals, ref.values)) < 1e-6
 
 
+@pytest.mark.parametrize("k,kq,n_other", [(2, 2, 12), (2, 4, 8), (4, 2, 6), (4, 4, 5)])
+def test_interleaved_broadcast_rows(ctx, k, kq, n_other):
+    """The tree's backward message: the parent variable xq is absent from the
+    big input and is the output's SLOWEST dim; the tile spans xq so one load of
+    the big values serves every row (output rows at xq's stride).  Compared
+    with the oracle's table (reference order) transposed to the planned layout."""
+    rng = random.Random(k * 1000 + kq * 100 + n_other)
+    xq, y = 0, 1
+    others = list(range(2, n_other + 2))
+    cards = {xq: kq, y: k}
+    for v in others:
+        cards[v] = rng.choice([2, 4])
+    cards[others[-1]] = 4
+    size = k
+    for v in others:
+        size *= cards[v]
+    big = (others + [y], [rng.uniform(0.5, 2.0) for _ in range(size)])
+    pair = ([xq, y], [rng.uniform(0.5, 2.0) for _ in range(kq * k)])
+    side = ([xq, others[-1]], [rng.uniform(0.5, 2.0) for _ in range(kq * 4)])
+    unary = ([xq], [rng.uniform(0.5, 2.0) for _ in range(kq)])
+    ins = [big, pair, side, unary]
+    fs = [refcpu.Factor.new(sc, cards, v) for sc, v in ins]
+    ref = refcpu.bucket(fs, y, cards[y])
+    planned = [xq] + others
+    t = torch.tensor(ref.values, dtype=torch.float64).reshape([cards[v] for v in ref.scope])
+    want = t.permute([ref.scope.index(v) for v in planned]).reshape(-1).tolist()
+    scope, vals = run_bucket(ctx, bnpp.F64, cards, ins, y, out_vars=planned)
+    assert scope == planned
+    assert vals == want
+    scope, vals = run_bucket(ctx, bnpp.F32, cards, ins, y, out_vars=planned)
+    assert max(abs(a - b) / abs(b) for a, b in zip(vals, want)) < 1e-6
+
+
 def test_permuted_output_layout(ctx):
     """Any permutation of the output scope is accepted and gives the same table, transposed."""
     rng = random.Random(5)
