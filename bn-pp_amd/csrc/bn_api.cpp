@@ -369,9 +369,15 @@ std::vector<const Factor *> Model::marginals(const std::unordered_map<unsigned, 
     for (auto pv : _variables) targets.push_back((int)pv->id());
     double up = 0;
     int dt = options["fp32"] ? BNPP_F32 : BNPP_F64;
-    check(bnpp_marginals(ctx(), g.m, (int)ev_vars.size(), ev_vars.data(), ev_vals.data(), heuristic_of(options),
-                         (int)targets.size(), targets.data(), dt, out.data(), &up),
-          "marginals");
+    if (options["bucket-tree"])                      // all marginals from one bucket tree (to rounding)
+        check(bnpp_marginals_tree(ctx(), g.m, (int)ev_vars.size(), ev_vars.data(), ev_vals.data(),
+                                  heuristic_of(options), nullptr, 0, (int)targets.size(), targets.data(), dt,
+                                  out.data(), &up),
+              "marginals (bucket tree)");
+    else                                             // one VE per target, bit-exact (model.cpp:326-334)
+        check(bnpp_marginals(ctx(), g.m, (int)ev_vars.size(), ev_vars.data(), ev_vals.data(), heuristic_of(options),
+                             (int)targets.size(), targets.data(), dt, out.data(), &up),
+              "marginals");
     std::vector<const Factor *> marg;
     size_t o = 0;
     for (auto pv : _variables) {

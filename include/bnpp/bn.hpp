@@ -109,6 +109,9 @@ public:
     // result is the same quantity)
     virtual double partition(const std::unordered_map<unsigned, unsigned> &evidence,
                              std::unordered_map<std::string, bool> &options, double &uptime) const;
+    // options["bucket-tree"]: all marginals from one two-pass bucket tree
+    // (bnpp_marginals_tree, equal to rounding); default: one VE per target,
+    // bit-exact with the reference arithmetic
     virtual std::vector<const Factor *> marginals(const std::unordered_map<unsigned, unsigned> &evidence,
                                                   std::unordered_map<std::string, bool> &options,
                                                   double &uptime) const;
