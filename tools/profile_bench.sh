@@ -1,5 +1,6 @@
-# rocprofv3 evidence for bench.py (run on the GPU box from the repo root):
-#   kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in separate PMC passes.
+# rocprofv3 evidence (run on the GPU box from the repo root):
+#   bench kernel trace + stats, FETCH_SIZE and WRITE_SIZE in separate PMC passes,
+#   the 32x32 bucket-tree MAR kernel stats, then the full bench line.
 set -e
 R=$PWD
 OUT=$R/gpurun_out/prof
@@ -9,5 +10,7 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-mar > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-mar > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-mar > $OUT/write.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/mar32 -o mar32 --output-format csv -- python3 $R/tools/mar_grid.py --rows 32 --cols 32 --check 0 > $OUT/mar32.log 2>&1
 cd $R
-timeout -k 10 300 python3 bench.py > $OUT/bench.log 2>&1
+python3 tools/pmc_traffic.py $(find $OUT/fetch -name "*counter_collection.csv") $(find $OUT/write -name "*counter_collection.csv") > $OUT/traffic.json
+timeout -k 10 600 python3 bench.py > $OUT/bench.log 2>&1
