@@ -194,7 +194,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
         plans.push_back(plan_bucket_tree(d.cards, views, ord, targets, part, n_parts));
-        auto need = [&](const VEPlan &p) { return plan_peak_bytes(p, eb) + (int64_t)p.buckets.size() * 512; };
+        auto need = [&](const VEPlan &p) { return plan_arena_bytes(p, eb) + (int64_t)p.buckets.size() * 512; };
         const char *force = std::getenv("BNPP_TREE_SLOTS");     // testing / tuning: chain mode, fixed slots
         if (force && std::atoi(force) > 0) {
             std::string msg;
@@ -260,7 +260,7 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     std::vector<std::vector<const VEPlan *>> batches(1);
     int64_t acc = 0;
     for (auto &p : plans) {
-        int64_t need = plan_peak_bytes(p, eb) + (int64_t)p.buckets.size() * 512;
+        int64_t need = (kind == 3 ? plan_arena_bytes(p, eb) : plan_peak_bytes(p, eb)) + (int64_t)p.buckets.size() * 512;
         if (kind == 3 && need > budget) {
             char m[256];
             std::snprintf(m, sizeof m, "bucket-tree marginals need %.2f GB, budget %.2f GB: the tree is not a "
@@ -284,6 +284,12 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
         entries += s.entries;
         moved += s.elems_moved;
         arena = std::max(arena, (double)s.arena_bytes);
+        if (timing) {
+            int64_t ideal = 0;
+            for (const VEPlan *pp : bp) ideal += plan_peak_bytes(*pp, eb);
+            std::fprintf(stderr, "[bnpp] schedule: %zu buckets, ideal live peak %.2f GB, arena %.2f GB\n",
+                         s.descs.size(), ideal / 1e9, s.arena_bytes / 1e9);
+        }
         levels += s.n_levels;
         buckets += (double)s.descs.size();
         out.push_back(std::move(s));

@@ -725,6 +725,27 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
     for (auto &pa : paths) total += (int64_t)pa.size();
     const int64_t g_lo = total * part / n_parts, g_hi = total * (part + 1) / n_parts;
     std::vector<char> owned_var(cards.size(), part == 0 ? 1 : 0);   // variables on no path: part 0
+    // Deliveries: positions j where lam_j * pi_j (the belief over sep_j) is
+    // formed.  One belief gives, in one pass that sums its slowest variables
+    // (a composite of card <= kSlowMax), a small table over its fastest
+    // variables (kept set K_j, <= kKeepMax entries); every owned target in K_j
+    // takes its marginal from that table.  The deliveries are a minimum set of
+    // positions stabbing every target's interval {j : x_q in K_j} (greedy by
+    // right end), so a 32-wide column sweep needs one delivery per ~20
+    // positions, and the forward messages are only recomputed to reach those.
+    const int64_t kKeepMax = (int64_t)1 << 21, kSlowMax = 8192;
+    auto slow_part = [&](const std::vector<int> &sep) {     // slowest vars summed in the first pass
+        std::vector<int> slow;
+        int64_t P = 1;
+        for (int v : sep) P *= cards[v];
+        int64_t sp = 1;
+        for (int v : sep) {
+            if (P / sp <= kKeepMax || sp * cards[v] > kSlowMax) break;
+            sp *= cards[v];
+            slow.push_back(v);
+        }
+        return slow;
+    };
     int64_t off = 0;
     for (const std::vector<int> &path : paths) {
         const int m = (int)path.size();
@@ -734,11 +755,54 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         off += m;
         if (a >= b) continue;
         for (int q = a; q < b; ++q) owned_var[order[path[q]]] = 1;
-        // backward sweep state: pi of path[j] (message from path[j+1] into path[j])
+        // kept sets K_j and the slow parts, per position
+        std::vector<std::vector<int>> slow(std::max(m - 1, 0));
+        for (int j = 0; j + 1 < m; ++j) slow[j] = slow_part(lam_vars[path[j]]);
+        auto kept = [&](int j, int v) {
+            const std::vector<int> &sep = lam_vars[path[j]];
+            if (std::find(sep.begin(), sep.end(), v) == sep.end()) return false;
+            return std::find(slow[j].begin(), slow[j].end(), v) == slow[j].end();
+        };
+        // targets x_q (q >= 1) and their intervals
+        struct Tgt { int q, lo, hi; };
+        std::vector<Tgt> tg;
+        std::map<int, std::vector<int>> multi, direct;       // delivery position -> targets
+        for (int q = std::max(a, 1); q < b; ++q) {
+            const int v = order[path[q]];
+            int lo = -1, hi = -1;
+            for (int j = q - 1; j >= 0; --j) {
+                const std::vector<int> &sep = lam_vars[path[j]];
+                if (std::find(sep.begin(), sep.end(), v) == sep.end()) break;
+                if (kept(j, v)) {
+                    if (hi < 0) hi = j;
+                    lo = j;
+                }
+            }
+            if (hi < 0) direct[q - 1].push_back(v);          // never in a kept set: its own reduction
+            else tg.push_back({q, lo, hi});
+        }
+        std::sort(tg.begin(), tg.end(), [](const Tgt &x, const Tgt &y) { return x.hi < y.hi; });
+        std::vector<char> done(tg.size(), 0);
+        for (size_t t = 0; t < tg.size(); ++t) {
+            if (done[t]) continue;
+            const int j = tg[t].hi;
+            for (size_t u = t; u < tg.size(); ++u)
+                if (!done[u] && tg[u].lo <= j && j <= tg[u].hi && kept(j, order[path[tg[u].q]])) {
+                    multi[j].push_back(order[path[tg[u].q]]);
+                    done[u] = 1;
+                }
+        }
+        std::vector<int> D;
+        for (auto &kv : multi) D.push_back(kv.first);
+        for (auto &kv : direct)
+            if (!multi.count(kv.first)) D.push_back(kv.first);
+        std::sort(D.begin(), D.end());
+        // backward sweep: pi_cur = pi_{pi_pos} (message from path[pi_pos + 1])
         View pi_cur;
         bool have_pi = false;                        // pi of the root: constant 1
-        // pi_j = sum F_{j+1} * pi_{j+1} down to sep_j (needs no forward message)
-        auto pi_step = [&](int j, const std::vector<int> &sep_j) {
+        int pi_pos = m - 1;
+        auto pi_step = [&](int j) {                  // pi_j = sum F_{j+1} * pi_{j+1} down to sep_j
+            const std::vector<int> &sep_j = lam_vars[path[j]];
             const int q = path[j + 1];
             std::vector<View> in = src_in[q];
             if (have_pi) in.push_back(pi_cur);
@@ -759,54 +823,75 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             }
             have_pi = true;
         };
-        // deliveries j in [lo, hi): marginal of x_{j+1} = lam_j * pi_j summed down to it
-        const int lo = std::max(a - 1, 0), hi = b - 1;
-        for (int j = m - 2; j >= std::max(hi, 0); --j) pi_step(j, lam_vars[path[j]]);   // suffix: pi only
-        int next_deliver = hi - 1;
-        auto deliver = [&](int j, const View &lam_j) {
-            if (j != next_deliver) return false;
-            pi_step(j, lam_j.vars);
+        auto pi_down_to = [&](int j) {
+            for (int jj = pi_pos - 1; jj >= j; --jj) pi_step(jj);
+            pi_pos = std::min(pi_pos, j);
+        };
+        int next_deliver = (int)D.size() - 1;
+        auto deliver = [&](int i, const View &lam_j) {
+            if (i != next_deliver) return false;
+            const int j = D[i];
+            pi_down_to(j);
             std::vector<View> bel{lam_j};
             if (have_pi) bel.push_back(pi_cur);
-            result_of[order[path[j + 1]]] = reduce_to(bel, order[path[j + 1]]);
+            auto mit = multi.find(j);
+            if (mit != multi.end()) {
+                int tb = -1;                                   // one pass: sum the slow vars
+                if (slow[j].size() >= 2) {
+                    std::vector<View> mg = bel;
+                    int vv = B.merge_group(mg, slow[j]);
+                    if (vv >= 0) tb = B.emit(mg, vv, false);
+                } else {
+                    tb = B.emit(bel, slow[j].empty() ? -1 : slow[j][0], false);
+                }
+                for (int t : mit->second)
+                    result_of[t] = tb >= 0 ? B.reduce_to({B.view(tb)}, t) : B.reduce_to(bel, t);
+            }
+            auto dit = direct.find(j);
+            if (dit != direct.end())
+                for (int t : dit->second) result_of[t] = B.reduce_to(bel, t);
             --next_deliver;
             return true;
         };
-        // reverse(lo, hi, start, s): deliver j = hi-1 ... lo; `start` = lam_{lo-1}
-        // (null for lo == 0), s free checkpoint slots (binomial checkpointing)
+        // lam at position `to` from lam at `from` (-1: from the path's start), streamed
+        auto advance = [&](const View *start, int from, int to) {
+            View cur = forward(path[from + 1], start);
+            for (int k = from + 2; k <= to; ++k) cur = forward(path[k], &cur);
+            return cur;
+        };
+        // reverse(lo, hi, start, spos, s): deliver D[hi-1] ... D[lo] (binomial
+        // checkpointing over the deliveries); `start` = lam at spos < D[lo]
         bool ok = true;
-        std::function<void(int, int, const View *, int)> reverse = [&](int rlo, int rhi, const View *start, int sl) {
+        std::function<void(int, int, const View *, int, int)> reverse = [&](int rlo, int rhi, const View *start,
+                                                                             int spos, int sl) {
             const int len = rhi - rlo;
             if (len <= 0 || !ok) return;
             if (len == 1 || sl <= 0) {
-                for (int j = rhi - 1; j >= rlo; --j) {        // stream lam_rlo..lam_j, deliver lam_j
-                    View cur = forward(path[rlo], start);
-                    for (int k = rlo + 1; k <= j; ++k) cur = forward(path[k], &cur);
-                    ok = ok && deliver(j, cur);
-                }
+                for (int i = rhi - 1; i >= rlo; --i) ok = ok && deliver(i, advance(start, spos, D[i]));
                 return;
             }
-            int r = 1;                                         // repetitions needed with sl slots
+            int r = 1;
             while (binom_capped(sl + r, sl) < len) ++r;
             int64_t right_cap = binom_capped(sl - 1 + r, sl - 1);
             int d = (int)std::max<int64_t>(1, len - std::min<int64_t>(right_cap, len - 1));
-            View ck = forward(path[rlo], start);               // advance d steps, keep lam_{rlo+d-1}
-            for (int k = rlo + 1; k < rlo + d; ++k) ck = forward(path[k], &ck);
             const int c = rlo + d - 1;
-            reverse(c + 1, rhi, &ck, sl - 1);
+            View ck = advance(start, spos, D[c]);
+            reverse(c + 1, rhi, &ck, D[c], sl - 1);
             ok = ok && deliver(c, ck);
-            reverse(rlo, c, start, sl);
+            reverse(rlo, c, start, spos, sl);
         };
-        if (hi > lo) {
-            View start;                                        // prefix: stream lam_0 .. lam_{lo-1}
-            for (int k = 0; k < lo; ++k) start = forward(path[k], k ? &start : nullptr);
-            reverse(lo, hi, lo ? &start : nullptr, slots);
+        if (!D.empty()) {
+            View start;                                        // prefix: stream to D[0] - 1, kept throughout
+            const int sp = D[0] - 1;
+            if (sp >= 0) start = advance(nullptr, -1, sp);
+            reverse(0, (int)D.size(), sp >= 0 ? &start : nullptr, sp, slots);
         }
-        if (!ok || next_deliver != lo - 1) {
+        if (!ok || next_deliver != -1) {
             if (msg) *msg = "internal: checkpoint schedule out of order";
             return false;
         }
         if (a == 0) {                                          // the leaf: its own bucket and pi_0
+            pi_down_to(0);
             std::vector<View> bel = src_in[path[0]];
             if (have_pi) bel.push_back(pi_cur);
             result_of[order[path[0]]] = reduce_to(bel, order[path[0]]);
@@ -855,13 +940,16 @@ struct Arena {
     int64_t top = 0;
     int64_t alloc(int64_t n) {
         n = (n + 255) & ~(int64_t)255;
-        for (auto it = free_.begin(); it != free_.end(); ++it) {
-            if (it->second >= n) {
-                int64_t off = it->first, len = it->second;
-                free_.erase(it);
-                if (len > n) free_[off + n] = len - n;
-                return off;
-            }
+        // best fit: the smallest free block that holds n (small temporaries go
+        // into small holes instead of splitting the holes big messages need)
+        auto best = free_.end();
+        for (auto it = free_.begin(); it != free_.end(); ++it)
+            if (it->second >= n && (best == free_.end() || it->second < best->second)) best = it;
+        if (best != free_.end()) {
+            int64_t off = best->first, len = best->second;
+            free_.erase(best);
+            if (len > n) free_[off + n] = len - n;
+            return off;
         }
         // extend: merge with a trailing free block if present
         if (!free_.empty()) {
@@ -895,6 +983,32 @@ struct Arena {
     }
 };
 }  // namespace
+
+int64_t plan_arena_bytes(const VEPlan &p, int elem_bytes) {
+    const int nt = p.n_src + (int)p.msgs.size();
+    std::vector<int> born(nt, 0), last(nt, -1);
+    for (const BucketSpec &b : p.buckets) {
+        born[b.out_table] = b.level;
+        for (const View &v : b.in) last[v.table] = std::max(last[v.table], b.level);
+    }
+    std::vector<char> keep(nt, 0);
+    if (p.result_table >= 0) keep[p.result_table] = 1;
+    for (int r : p.results)
+        if (r >= 0) keep[r] = 1;
+    std::vector<std::vector<int>> born_at(p.n_levels + 2), dies_at(p.n_levels + 2);
+    for (int t = p.n_src; t < nt; ++t) {
+        born_at[born[t]].push_back(t);
+        if (!keep[t]) dies_at[std::max(last[t], born[t])].push_back(t);
+    }
+    Arena arena;
+    std::vector<int64_t> off(nt, 0);
+    auto bytes = [&](int t) { return p.msgs[t - p.n_src].size * elem_bytes; };
+    for (int L = 1; L <= p.n_levels; ++L) {
+        for (int t : born_at[L]) off[t] = arena.alloc(bytes(t));
+        for (int t : dies_at[L]) arena.release(off[t], bytes(t));
+    }
+    return arena.top;
+}
 
 bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<int> &cards,
                     const std::vector<int64_t> &src_sizes, int elem_bytes, int max_vec, Schedule &s,

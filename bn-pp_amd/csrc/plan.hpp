@@ -136,6 +136,9 @@ struct Schedule {
 
 // Peak bytes of live messages when the plan runs level by level (arena estimate).
 int64_t plan_peak_bytes(const VEPlan &p, int elem_bytes);
+// Bytes of the arena build_schedule allocates for this plan alone (the same
+// best-fit allocator, so fragmentation included).
+int64_t plan_arena_bytes(const VEPlan &p, int elem_bytes);
 
 bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<int> &cards,
                     const std::vector<int64_t> &src_sizes, int elem_bytes, int max_vec, Schedule &s,
