@@ -444,7 +444,7 @@ int bnpp_ctx_create(int device, bnpp_ctx **out) {
     if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return set_err(BNPP_ERR_HIP, hipGetErrorString(e));
     std::unique_ptr<bnpp_ctx> ctx(new bnpp_ctx);
     ctx->c.device = device;
-    int per_cu = 8;
+    int per_cu = 3;          // measured: 3 workgroups per CU beat 4 and 8 on the bench bucket and the 32x32 sweep
     if (const char *g = std::getenv("BNPP_GRID_PER_CU")) per_cu = std::max(1, std::min(64, std::atoi(g)));
     ctx->c.max_grid = prop.multiProcessorCount * per_cu;
     if ((e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking)) != hipSuccess)

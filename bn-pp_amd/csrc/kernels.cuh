@@ -261,21 +261,40 @@ constexpr int kLdsWaveBytes = 64 * (64 + kLdsRowPad);      // largest tile: 64 B
 // output entries [tid*TS, tid*TS + TS)).  Tiles of one 16-B access are stored
 // directly (already coalesced); wider tiles go through the wave's LDS image so
 // every global store instruction writes 64 consecutive 16-B chunks.
+#ifndef BNPP_WAVE_SYNC
+#define BNPP_WAVE_SYNC 0
+#endif
+#ifndef BNPP_DIRECT_STORE
+#define BNPP_DIRECT_STORE 0
+#endif
+// the LDS image is private to one wave: ordering its writes and reads needs
+// only the wave itself (LDS executes a wave's instructions in order), not the
+// workgroup barrier
+__device__ __forceinline__ void image_sync() {
+    if constexpr (BNPP_WAVE_SYNC != 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 template <typename T, int TS>
 __device__ __forceinline__ void store_tiles(T *out, int64_t wave_tid0, int64_t n_tiles, const T (&acc)[TS],
                                             unsigned char *lds) {
     const int lane = threadIdx.x & 63;
     const int64_t tid = wave_tid0 + lane;
     constexpr int row_bytes = TS * (int)sizeof(T);
-    if constexpr (row_bytes <= 16) {
+    if constexpr (row_bytes <= 16 || BNPP_DIRECT_STORE != 0) {
         if (tid < n_tiles) store_n<T, TS, kNtStore>(out + tid * TS, acc);
     } else {
         constexpr int rowp = row_bytes + kLdsRowPad;
         constexpr int cpr = row_bytes / 16;                   // 16-B chunks per row
         constexpr int EPC = 16 / (int)sizeof(T);              // entries per chunk
-        __syncthreads();                                      // previous reads of this image are done
+        image_sync();                                         // previous reads of this image are done
         store_n<T, TS>(reinterpret_cast<T *>(lds + lane * rowp), acc);
-        __syncthreads();
+        image_sync();
         const int64_t valid = n_tiles - wave_tid0;            // tiles of this wave that exist
 #pragma unroll
         for (int it = 0; it < cpr; ++it) {
