@@ -60,6 +60,9 @@ struct BucketDesc {
     int32_t small_elems;            // LDS elements for the small inputs
     int32_t in_lds_off[kMaxIn];     // element offset of each small input in LDS
     int32_t in_span[kMaxIn];        // elements of each small input's reachable range
+    // chain form (chain != 0): F consecutive buckets of a sweep fused in
+    // registers; chain = F | gmask << 8 | form << 16 (bnpp_device.h, ChainForm)
+    int32_t chain, chain_pad;
 };
 
 // arguments of one level launch (a group of buckets of one kernel variant)
@@ -85,6 +88,25 @@ __host__ __device__ inline int nin_class(int n_in) { return n_in <= 1 ? 1 : n_in
 __host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return nin_class(n_in) * 64 + v1 * 8 + v2; }
 // stream kernels: 4096 + big-class * 256 + v1 * 16 + v2  (v1, v2 <= 8)
 __host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 256 + v1 * 16 + v2; }
+
+// Chain (sweep) form: F consecutive buckets of an elimination chain in one
+// pass.  Input 0 is the message entering the run; bucket j of the run sums
+// slot variable x_j out of a K^F register table and puts its new variable n_j
+// in the same slot, multiplying by G_j (the product of bucket j's factor
+// tables, inputs 1.. in order, present when bit j of gmask is set).
+//   kChainFwd: x_j are the input's slowest variables (one slab per slot
+//              assignment), n_j the output's fastest block (per-thread row of
+//              K^F entries, stored through the wave's LDS image)
+//   kChainBwd: x_j are the input's fastest variables (slot 0 fastest: one
+//              contiguous K^F block per entry of the rest), the output holds
+//              n_j at slab strides; 16 B of the rest's fastest dim per thread
+enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2 };
+__host__ __device__ inline int chain_key(int form, int k, int f) { return 8192 + form * 256 + k * 16 + f; }
+// chain pool rows: per rest dim (fastest first) 4 + F words
+//   w0 header  w1 magic  w2 input stride  w3 output stride  w4.. G_j stride (j < F)
+// then per slot p: input stride, output stride (2F words); then per bucket j:
+// G_j strides of the variable in every slot at that bucket (slot j: x_j), and
+// of n_j (F * (F + 1) words)
 
 // dims pool, per output dim (fastest first): 2 + n_in int64 words
 //   w0 = card | (shift << 32) | (pow2 << 40)    w1 = magic    w2.. = stride per input

@@ -194,12 +194,14 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
         plans.push_back(plan_bucket_tree(d.cards, views, ord, targets, part, n_parts));
+        const char *nc = std::getenv("BNPP_NO_CHAIN");             // A/B: unfused sweeps
+        const int chain_eb = nc && *nc == '1' ? 0 : eb;
         auto need = [&](const VEPlan &p) { return plan_arena_bytes(p, eb) + (int64_t)p.buckets.size() * 512; };
         const char *force = std::getenv("BNPP_TREE_SLOTS");     // testing / tuning: chain mode, fixed slots
         if (force && std::atoi(force) > 0) {
             std::string msg;
             VEPlan cp;
-            if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), part, n_parts, cp, &msg))
+            if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), part, n_parts, cp, &msg, chain_eb))
                 return set_err(BNPP_ERR_UNSUPPORTED, msg);
             plans.back() = std::move(cp);
         } else if (need(plans.back()) > budget || n_parts > 1) {
@@ -211,7 +213,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             while (lo <= hi) {
                 int mid = (lo + hi) / 2;
                 VEPlan cp;
-                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, part, n_parts, cp, &msg)) break;
+                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, part, n_parts, cp, &msg, chain_eb)) break;
                 if (need(cp) <= budget) {
                     best_s = mid;
                     best = std::move(cp);

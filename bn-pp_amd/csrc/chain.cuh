@@ -1,0 +1,301 @@
+// Chain (sweep) kernels: F consecutive buckets of an elimination chain fused
+// into one pass over the message (bnpp_device.h, ChainForm).
+//
+// In a sweep (the column-sweep order on a grid, the forward and backward
+// passes of the bucket tree) bucket q's only large input is bucket q-1's
+// message, and it swaps one variable of the message for one new variable:
+//     msg_q(rest, n_q) = sum_{x_q} G_q(x_q, n_q, ...) * msg_{q-1}(x_q, rest)
+// (model.cpp:414-418 with G_q = Factor(1.0) *= the bucket's factor tables).
+// Run one bucket per launch and every message crosses HBM twice (written,
+// read back).  Here one thread owns K^F entries of the run's input (the
+// assignments of its F summed variables for one entry of the rest), runs the
+// F buckets on them in registers -- each in the reference's arithmetic order,
+// p = G_q * msg, acc = 0; acc += p for x_q = 0..K-1 (factor.cpp:131-143,
+// 199-205) -- and writes the run's output once: HBM traffic per bucket / F.
+// The intermediate messages are exactly the unfused ones (up to the power-of-
+// two scale, which is applied once at the end), so fp64 stays bit-identical.
+#pragma once
+#include <type_traits>
+#include <utility>
+
+#include "kernels.cuh"
+
+namespace bnpp {
+
+__host__ __device__ constexpr int ipow(int k, int f) { return f == 0 ? 1 : k * ipow(k, f - 1); }
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [0, N) -- the
+// register table must only ever be indexed by constants (else it goes to scratch)
+template <int I, int N, typename Fn>
+__device__ __forceinline__ void static_for_impl(Fn &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for_impl<I + 1, N>(f);
+    }
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn &&f) { static_for_impl<0, N>(f); }
+
+template <int K, int F>
+struct ChainShape {
+    static constexpr int N = ipow(K, F);
+    // digit of slot p in register index a (slot 0 most significant)
+    static __device__ __forceinline__ constexpr int digit(int a, int p) { return (a / ipow(K, F - 1 - p)) % K; }
+    static __device__ __forceinline__ constexpr int place(int p) { return ipow(K, F - 1 - p); }
+    // memory position of register index a in a block whose slot 0 is fastest
+    static __device__ __forceinline__ constexpr int rev(int a) {
+        int r = 0;
+        for (int p = 0; p < F; ++p) r += digit(a, p) * ipow(K, p);
+        return r;
+    }
+};
+
+template <int F>
+struct ChainState {
+    const void *big;
+    void *out;
+    const int64_t *dims;
+    int64_t n_tiles, in_base;
+    int64_t t0h, t0m;
+    int64_t is[F], os[F];
+    int32_t gs[F][F], gsn[F], glds[F];
+    int n_dims, gmask, flags, neg_e;
+};
+
+template <typename T, int K, int F, int FORM>
+__device__ __forceinline__ void chain_load_state(ChainState<F> &c, const BucketDesc &d, const int64_t *pool,
+                                                 TableMeta *meta) {
+    c.dims = pool;
+    c.n_dims = d.n_dims;
+    c.n_tiles = d.n_tiles;
+    c.t0h = d.tdiv0[0];
+    c.t0m = d.tdiv0[1];
+    c.gmask = (d.chain >> 8) & 0xff;
+    c.flags = d.flags;
+    c.in_base = d.in_base[0];
+    const int row = 4 + F;
+    const int64_t *sl = pool + (int64_t)d.n_dims * row;
+#pragma unroll
+    for (int p = 0; p < F; ++p) {
+        c.is[p] = sl[2 * p];
+        c.os[p] = sl[2 * p + 1];
+    }
+    const int64_t *st = sl + 2 * F;
+    int gi = 1;
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+#pragma unroll
+        for (int p = 0; p < F; ++p) c.gs[j][p] = (int32_t)st[j * (F + 1) + p];
+        c.gsn[j] = (int32_t)st[j * (F + 1) + F];
+        const bool on = (c.gmask >> j) & 1;
+        c.glds[j] = on ? d.in_lds_off[gi] : 0;
+        gi += on ? 1 : 0;
+    }
+    c.big = meta[d.in_table[0]].ptr;
+    c.out = meta[d.out_table].ptr;
+    int64_t e_sum = 0, x_sum = 0;
+    for (int i = 0; i < kMaxIn; ++i) {
+        if (i >= d.n_in) break;
+        const TableMeta &mi = meta[d.in_table[i]];
+        const int e = FBits<T>::exponent(mi.maxbits);
+        if (d.flags & kScale) {
+            e_sum += e;
+            x_sum += mi.exp2 + e;
+        } else {
+            x_sum += mi.exp2;
+        }
+    }
+    c.neg_e = (int)(-e_sum);
+    (void)x_sum;
+}
+
+template <typename T>
+__device__ __forceinline__ int64_t chain_exp2(const BucketDesc &d, TableMeta *meta) {
+    int64_t x_sum = 0;
+    for (int i = 0; i < kMaxIn; ++i) {
+        if (i >= d.n_in) break;
+        const TableMeta &mi = meta[d.in_table[i]];
+        x_sum += mi.exp2 + ((d.flags & kScale) ? FBits<T>::exponent(mi.maxbits) : 0);
+    }
+    return x_sum;
+}
+
+// copy the G tables of the run into LDS (uniform control flow)
+template <typename T>
+__device__ __forceinline__ void chain_stage(const BucketDesc &d, TableMeta *meta, T *small) {
+    __syncthreads();
+    for (int i = 1; i < kMaxIn; ++i) {
+        if (i >= d.n_in) break;
+        const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
+        const int off = d.in_lds_off[i], span = d.in_span[i];
+        for (int e = threadIdx.x; e < span; e += kBlock) small[off + e] = src[e];
+    }
+    __syncthreads();
+}
+
+template <typename T, int K, int F, int FORM>
+__global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
+                                                             const int64_t *__restrict__ pool,
+                                                             TableMeta *__restrict__ meta, int64_t total_vblocks) {
+    using S = ChainShape<K, F>;
+    constexpr int N = S::N;
+    constexpr int V = FORM == kChainFwd ? 1 : 16 / (int)sizeof(T);   // entries of the rest per thread
+    static_assert(FORM != kChainFwd || N * (int)sizeof(T) <= 64, "forward rows go through the 64-B LDS image");
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    T *red = reinterpret_cast<T *>(dyn);
+    unsigned char *stage = dyn + kRedBytes;
+    constexpr int kImg = FORM == kChainFwd ? (kBlock / 64) * kLdsWaveBytes : 0;
+    T *small = reinterpret_cast<T *>(dyn + kRedBytes + kImg);
+
+    ChainState<F> c;
+    int cur = -1;
+    int64_t cur_begin = 0;
+    T lmax = T(0);
+    for (int64_t vb = blockIdx.x; vb < total_vblocks; vb += gridDim.x) {
+        const int bi = n_desc == 1 ? 0 : find_bucket(descs, n_desc, vb);
+        if (bi != cur) {
+            if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
+            cur = bi;
+            lmax = T(0);
+            const BucketDesc &d = descs[bi];
+            cur_begin = d.vblk_begin;
+            chain_load_state<T, K, F, FORM>(c, d, pool + d.dim_off, meta);
+            if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta);
+            chain_stage<T>(d, meta, small);
+        }
+        const int64_t tid0 = (vb - cur_begin) * kBlock;
+        const int64_t tid = tid0 + threadIdx.x;
+        T t[N][V];
+        if (tid < c.n_tiles) {
+            // rest position of this thread: in / out offsets, G offsets in LDS
+            const int row = 4 + F;
+            const int64_t *dp = c.dims;
+            int64_t in_off = c.in_base, out_off = 0;
+            int32_t gb[F], gv[F];
+            uint64_t q, r;
+            divmod_dim((uint64_t)tid, c.t0h, c.t0m, q, r);
+            const int64_t i0 = (int64_t)r * V;
+            in_off += i0 * dp[2];
+            out_off += i0 * dp[3];
+            const int64_t in_v = dp[2];
+#pragma unroll
+            for (int j = 0; j < F; ++j) {
+                gv[j] = (int32_t)dp[4 + j];
+                gb[j] = c.glds[j] + (int32_t)i0 * gv[j];
+            }
+            uint64_t rem = q;
+            dp += row;
+            for (int dd = 1; dd < c.n_dims; ++dd) {
+                uint64_t qq, rr;
+                divmod_dim(rem, dp[0], dp[1], qq, rr);
+                in_off += (int64_t)rr * dp[2];
+                out_off += (int64_t)rr * dp[3];
+#pragma unroll
+                for (int j = 0; j < F; ++j) gb[j] += (int32_t)rr * (int32_t)dp[4 + j];
+                rem = qq;
+                dp += row;
+            }
+            const T *big = static_cast<const T *>(c.big);
+            if constexpr (FORM == kChainFwd) {
+                // one slab per slot assignment: scalar loads, coalesced over the wave
+#pragma unroll
+                for (int a = 0; a < N; ++a) {
+                    int64_t o = in_off;
+#pragma unroll
+                    for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.is[p];
+                    t[a][0] = big[o];
+                }
+            } else {
+                // K^F contiguous entries (slot 0 fastest) per rest entry
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    T buf[N];
+                    load_n<T, N, kNtLoad>(big + in_off + v * in_v, buf);
+#pragma unroll
+                    for (int a = 0; a < N; ++a) t[a][v] = buf[S::rev(a)];
+                }
+            }
+            // the F buckets of the run, in order
+            static_for<F>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                const bool has_g = (c.gmask >> j) & 1;           // uniform
+                static_for<N>([&](auto ac) {
+                    constexpr int a = decltype(ac)::value;
+                    if constexpr (S::digit(a, j) == 0) {
+                        int32_t go = gb[j];
+#pragma unroll
+                        for (int p = 0; p < F; ++p)
+                            if (p != j) go += S::digit(a, p) * c.gs[j][p];
+                        T nw[K][V];
+#pragma unroll
+                        for (int n = 0; n < K; ++n) {
+#pragma unroll
+                            for (int v = 0; v < V; ++v) nw[n][v] = T(0);
+#pragma unroll
+                            for (int x = 0; x < K; ++x) {
+#pragma unroll
+                                for (int v = 0; v < V; ++v) {
+                                    const T m = t[a + x * S::place(j)][v];
+                                    const T p = has_g ? small[go + x * c.gs[j][j] + n * c.gsn[j] + v * gv[j]] * m : m;
+                                    nw[n][v] = nw[n][v] + p;
+                                }
+                            }
+                        }
+#pragma unroll
+                        for (int n = 0; n < K; ++n)
+#pragma unroll
+                            for (int v = 0; v < V; ++v) t[a + n * S::place(j)][v] = nw[n][v];
+                    }
+                });
+            });
+            if (c.flags & kScale) {
+#pragma unroll
+                for (int a = 0; a < N; ++a)
+#pragma unroll
+                    for (int v = 0; v < V; ++v) t[a][v] = ldexp_t(t[a][v], c.neg_e);
+            }
+#pragma unroll
+            for (int a = 0; a < N; ++a)
+#pragma unroll
+                for (int v = 0; v < V; ++v) lmax = t[a][v] > lmax ? t[a][v] : lmax;
+            if constexpr (FORM == kChainBwd) {
+                T *out = static_cast<T *>(c.out);
+#pragma unroll
+                for (int a = 0; a < N; ++a) {
+                    int64_t o = out_off;
+#pragma unroll
+                    for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.os[p];
+                    store_n<T, V, kNtStore>(out + o, t[a]);
+                }
+            }
+        }
+        if constexpr (FORM == kChainFwd) {
+            // the thread's K^F outputs are the contiguous row tid (planner-checked)
+            T row[N];
+#pragma unroll
+            for (int a = 0; a < N; ++a) row[a] = t[a][0];
+            store_tiles<T, N>(static_cast<T *>(c.out), tid0 + (threadIdx.x & ~63), c.n_tiles, row,
+                              stage + (threadIdx.x >> 6) * kLdsWaveBytes);
+        }
+    }
+    if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
+}
+
+template <typename T, int K, int F, int FORM>
+static hipError_t go_chain_level(const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream) {
+    const int64_t grid = a.vblocks < max_grid ? a.vblocks : max_grid;
+    const size_t img = FORM == kChainFwd ? (size_t)(kBlock / 64) * kLdsWaveBytes : 0;
+    const size_t shm = kRedBytes + img + (size_t)small_elems * sizeof(T);
+    hipLaunchKernelGGL((chain_level_kernel<T, K, F, FORM>), dim3((unsigned)grid), dim3(kBlock), shm, stream, a.descs,
+                       a.n_desc, a.pool, a.meta, a.vblocks);
+    return hipGetLastError();
+}
+
+#define BNPP_CASE_CHAIN(T, K, F, FORM) \
+    case 8192 + FORM * 256 + K * 16 + F: return go_chain_level<T, K, F, FORM>(a, small_elems, max_grid, stream);
+// instantiated shapes (planner: kChainMaxN per dtype)
+#define BNPP_CHAIN_F32(X, T) X(T, 2, 2, 1) X(T, 2, 3, 1) X(T, 2, 4, 1) X(T, 4, 2, 1) \
+    X(T, 2, 2, 2) X(T, 2, 3, 2) X(T, 2, 4, 2) X(T, 4, 2, 2)
+#define BNPP_CHAIN_F64(X, T) X(T, 2, 2, 1) X(T, 2, 3, 1) X(T, 2, 2, 2) X(T, 2, 3, 2)
+
+}  // namespace bnpp

@@ -1,0 +1,10 @@
+// Chain (sweep) kernel instantiations, double (separate translation unit).
+#include "chain.cuh"
+
+namespace bnpp {
+
+hipError_t dispatch_chain_level_f64(int key, const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream) {
+    switch (key) { BNPP_CHAIN_F64(BNPP_CASE_CHAIN, double) default: break; }
+    return hipErrorInvalidValue;
+}
+}  // namespace bnpp

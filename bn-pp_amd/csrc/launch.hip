@@ -16,6 +16,9 @@ hipError_t dispatch_stream_single_f32(int key, const SingleArgs &a, int max_grid
 hipError_t dispatch_stream_level_f64(int key, const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream);
 hipError_t dispatch_stream_single_f64(int key, const SingleArgs &a, int max_grid, hipStream_t stream);
 
+hipError_t dispatch_chain_level_f32(int key, const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream);
+hipError_t dispatch_chain_level_f64(int key, const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream);
+
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream) {
     if (a.d.n_tiles <= 0) return hipSuccess;
     if (a.d.big >= 0) {
@@ -31,6 +34,9 @@ hipError_t launch_level(int is_f32, int variant, const BucketDesc *descs, int n_
                         TableMeta *meta, int64_t total_vblocks, int small_elems, int max_grid, hipStream_t stream) {
     if (n_desc <= 0 || total_vblocks <= 0) return hipSuccess;
     LevelArgs a{descs, n_desc, pool, meta, total_vblocks};
+    if (variant >= 8192)
+        return is_f32 ? dispatch_chain_level_f32(variant, a, small_elems, max_grid, stream)
+                      : dispatch_chain_level_f64(variant, a, small_elems, max_grid, stream);
     if (variant >= 4096)
         return is_f32 ? dispatch_stream_level_f32(variant, a, small_elems, max_grid, stream)
                       : dispatch_stream_level_f64(variant, a, small_elems, max_grid, stream);

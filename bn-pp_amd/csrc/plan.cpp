@@ -5,6 +5,7 @@
 #include <atomic>
 #include <thread>
 #include <climits>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -114,8 +115,163 @@ void magic_for(uint32_t d, uint32_t &shift, uint32_t &magic, bool &pow2) {
 }
 }  // namespace
 
+// Descriptor of a fused chain run (chain.cuh).  Returns false when the run's
+// layout fits neither kernel form.
+static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec, BucketDesc &d,
+                             std::vector<int64_t> &pool, std::string *msg) {
+    auto fail = [&](const char *m) {
+        if (msg) *msg = m;
+        return false;
+    };
+    const int F = (int)b.chain_x.size();
+    if (F < 1 || (int)b.chain_n.size() != F || b.in.empty()) return fail("chain: bad run");
+    const int K = cards[b.chain_x[0]];
+    const int eb = max_vec == 2 ? 8 : 4;
+    int N = 1;
+    for (int j = 0; j < F; ++j) {
+        if (cards[b.chain_x[j]] != K || cards[b.chain_n[j]] != K) return fail("chain: mixed cardinalities");
+        N *= K;
+    }
+    if (N > chain_max_entries(eb) || (K != 2 && K != 4)) return fail("chain: register table too large");
+    std::vector<int> gidx(F, -1);                     // input index of G_j (-1: absent)
+    int ni = 1;
+    for (int j = 0; j < F; ++j)
+        if ((b.chain_gmask >> j) & 1) gidx[j] = ni++;
+    if (ni != (int)b.in.size() || ni > kMaxIn) return fail("chain: G tables do not match the mask");
+    auto stride_of = [](const View &v, int var) -> int64_t {
+        for (size_t i = 0; i < v.vars.size(); ++i)
+            if (v.vars[i] == var) return v.strides[i];
+        return 0;
+    };
+    const View &big = b.in[0];
+    std::vector<int64_t> ostr = natural_strides(b.out_vars, cards);
+    auto out_stride = [&](int var) -> int64_t {
+        for (size_t i = 0; i < b.out_vars.size(); ++i)
+            if (b.out_vars[i] == var) return ostr[i];
+        return -1;
+    };
+    std::vector<int64_t> is(F), os(F);
+    for (int p = 0; p < F; ++p) {
+        is[p] = stride_of(big, b.chain_x[p]);
+        os[p] = out_stride(b.chain_n[p]);
+        if (is[p] <= 0 || os[p] < 0) return fail("chain: slot variable missing");
+    }
+    // rest dims (fastest first by output stride): in, out, G_j strides
+    struct RDim { uint64_t card; int64_t in, out; int64_t g[8]; };
+    std::vector<RDim> rd;
+    for (size_t i = b.out_vars.size(); i-- > 0;) {
+        const int v = b.out_vars[i];
+        if (std::find(b.chain_n.begin(), b.chain_n.end(), v) != b.chain_n.end() || cards[v] == 1) continue;
+        RDim r{(uint64_t)cards[v], stride_of(big, v), ostr[i], {0}};
+        if (r.in == 0) return fail("chain: rest variable missing from the message");
+        for (int j = 0; j < F; ++j) r.g[j] = gidx[j] >= 0 ? stride_of(b.in[gidx[j]], v) : 0;
+        rd.push_back(r);
+    }
+    std::vector<RDim> md;                             // merged
+    for (const RDim &r : rd) {
+        if (!md.empty()) {
+            RDim &bk = md.back();
+            const int64_t c = (int64_t)bk.card;
+            bool ok = bk.card * r.card <= (uint64_t)INT32_MAX && r.in == bk.in * c && r.out == bk.out * c;
+            for (int j = 0; ok && j < F; ++j) ok = r.g[j] == bk.g[j] * c;
+            if (ok) {
+                bk.card *= r.card;
+                continue;
+            }
+        }
+        md.push_back(r);
+    }
+    int64_t rest = 1;
+    for (const RDim &r : md) rest *= (int64_t)r.card;
+    // kernel form
+    int form = 0, V = 1;
+    {
+        bool fwd = N * eb <= 64;
+        for (int p = 0; fwd && p < F; ++p) {
+            int64_t pl = 1;
+            for (int q = p + 1; q < F; ++q) pl *= K;
+            fwd = os[p] == pl;
+        }
+        if (fwd && !md.empty()) fwd = md[0].out == N;
+        bool bwd = true;
+        const int W = eb == 4 ? (N % 4 == 0 ? 4 : N % 2 == 0 ? 2 : 1) : (N % 2 == 0 ? 2 : 1);   // load_n width
+        const int bv = 16 / eb;
+        int64_t pk = 1;
+        for (int p = 0; bwd && p < F; ++p, pk *= K) bwd = is[p] == pk;
+        bwd = bwd && !md.empty() && md[0].out == 1 && md[0].card % (uint64_t)bv == 0 && big.base % W == 0;
+        for (const RDim &r : md) bwd = bwd && r.in % W == 0 && (r.out % bv == 0 || &r == &md[0]);
+        for (int p = 0; bwd && p < F; ++p) bwd = os[p] % bv == 0;
+        if (fwd) form = kChainFwd;
+        else if (bwd) { form = kChainBwd; V = bv; }
+        else return fail("chain: layout fits no kernel form");
+    }
+    d = BucketDesc{};
+    d.out_size = rest * N;
+    d.n_tiles = rest / V;
+    d.v1 = V;
+    d.v2 = 1;
+    d.n_in = ni;
+    d.n_dims = (int)md.size();
+    d.k = K;
+    d.out_table = b.out_table;
+    d.flags = kScale | kTrackMax;
+    d.big = -1;
+    d.chain = F | (b.chain_gmask << 8) | (form << 16);
+    int32_t lo = 0;
+    for (int i = 0; i < kMaxIn; ++i) {
+        d.in_table[i] = i < ni ? b.in[i].table : 0;
+        d.in_base[i] = i < ni ? b.in[i].base : 0;
+        if (i >= 1 && i < ni) {
+            int64_t sp = 1;
+            for (size_t q = 0; q < b.in[i].vars.size(); ++q)
+                sp += (int64_t)(cards[b.in[i].vars[q]] - 1) * b.in[i].strides[q];
+            if (sp > kStreamSmallMax) return fail("chain: G table too large for LDS");
+            d.in_span[i] = (int32_t)sp;
+            d.in_lds_off[i] = lo;
+            lo += (int32_t)((sp + 3) & ~3);
+        }
+    }
+    d.small_elems = lo;
+    if ((int64_t)lo * eb > kStreamLdsBudget) return fail("chain: G tables exceed the LDS budget");
+    {
+        uint32_t shift, magic;
+        bool pow2;
+        const uint64_t c0 = md.empty() ? 1 : md[0].card / (uint64_t)V;
+        magic_for((uint32_t)c0, shift, magic, pow2);
+        d.tdiv0[0] = pack_dim_header((uint32_t)c0, shift, pow2);
+        d.tdiv0[1] = (int64_t)magic;
+        d.tdiv1[0] = pack_dim_header(1, 0, true);
+        d.tdiv1[1] = 0;
+    }
+    d.dim_off = (int64_t)pool.size();
+    for (const RDim &r : md) {
+        uint32_t shift, magic;
+        bool pow2;
+        magic_for((uint32_t)r.card, shift, magic, pow2);
+        pool.push_back(pack_dim_header((uint32_t)r.card, shift, pow2));
+        pool.push_back((int64_t)magic);
+        pool.push_back(r.in);
+        pool.push_back(r.out);
+        for (int j = 0; j < F; ++j) pool.push_back(r.g[j]);
+    }
+    for (int p = 0; p < F; ++p) {
+        pool.push_back(is[p]);
+        pool.push_back(os[p]);
+    }
+    for (int j = 0; j < F; ++j) {
+        const View *g = gidx[j] >= 0 ? &b.in[gidx[j]] : nullptr;
+        for (int p = 0; p < F; ++p) {
+            const int var = p < j ? b.chain_n[p] : b.chain_x[p];
+            pool.push_back(g ? stride_of(*g, var) : 0);
+        }
+        pool.push_back(g ? stride_of(*g, b.chain_n[j]) : 0);
+    }
+    return true;
+}
+
 bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec, BucketDesc &d,
                 std::vector<int64_t> &pool, std::string *msg) {
+    if (!b.chain_x.empty()) return build_chain_desc(b, cards, max_vec, d, pool, msg);
     const int n = (int)b.in.size();
     if (n < 1 || n > kMaxIn) {
         if (msg) *msg = "bucket needs 1.." + std::to_string(kMaxIn) + " inputs, got " + std::to_string(n);
@@ -411,13 +567,13 @@ struct PlanBuilder {
         for (const View &v : in) e += (double)table_size(v.vars, cards);
         return e;
     }
-    int push_bucket(const std::vector<View> &in, int x, const std::vector<int> &ov) {
+    int push_bucket(const std::vector<View> &in, int x, const std::vector<int> &ov, bool free_level = false) {
         BucketSpec b;
         b.in = in;
         b.elim_var = x;
         b.out_vars = ov;
         b.out_table = new_msg(ov);
-        int lv = sequential ? last_level : 0;
+        int lv = sequential && !free_level ? last_level : 0;
         for (const View &v : in) lv = std::max(lv, level[v.table]);
         b.level = lv + 1;
         last_level = std::max(last_level, b.level);
@@ -445,6 +601,92 @@ struct PlanBuilder {
         int t = push_bucket(in, x, ov);
         p.width = std::max(p.width, (int)ov.size());
         return t;
+    }
+    // ---- fused chain runs (chain.cuh) ----
+    int chain_eb = 0;                                   // element bytes of the run's dtype (0: no fusion)
+    std::map<std::vector<int64_t>, int> gcache;         // G product tables, by their factor views
+    struct ChainStep {
+        std::vector<View> smalls;                       // the bucket's factor tables, chain order
+        int x;                                          // the variable it sums out
+    };
+    // Buckets steps[0..F) as one fused run over the message `big` (each
+    // bucket's chain is smalls..., then the message, model.cpp:414-418).
+    // Returns the run's output table, or -1 when the run does not fit a
+    // chain kernel (the caller then emits the buckets one by one).
+    int emit_chain(const View &big, const std::vector<ChainStep> &steps) {
+        const int F = (int)steps.size();
+        if (chain_eb == 0 || F < 2) return -1;
+        std::vector<int> vars = big.vars, xs, ns;
+        for (const ChainStep &st : steps) {
+            std::vector<int> u = vars;
+            for (const View &v : st.smalls) {
+                if (table_size(v.vars, cards) > kStreamSmallMax) return -1;
+                for (int w : v.vars)
+                    if (!contains(u, w)) u.push_back(w);
+            }
+            if (!contains(vars, st.x) || !contains(big.vars, st.x) || contains(ns, st.x)) return -1;
+            std::vector<int> nw;
+            for (int w : u)
+                if (!contains(vars, w)) nw.push_back(w);
+            if (nw.size() != 1 || nw[0] == st.x) return -1;
+            xs.push_back(st.x);
+            ns.push_back(nw[0]);
+            vars = remove_var(u, st.x);
+        }
+        BucketSpec b;
+        b.in.push_back(big);
+        b.out_vars = canon(vars);
+        b.chain_x = xs;
+        b.chain_n = ns;
+        std::vector<int> prod_of;                       // input index -> step whose smalls need a product
+        for (int j = 0; j < F; ++j) {
+            const std::vector<View> &sm = steps[j].smalls;
+            if (sm.empty()) continue;
+            b.chain_gmask |= 1 << j;
+            if (sm.size() == 1) {
+                b.in.push_back(sm[0]);
+                prod_of.push_back(-1);
+            } else {
+                b.in.push_back(natural_view(-1, canon(chain_scope(sm)), cards));
+                prod_of.push_back(j);
+            }
+        }
+        {
+            BucketDesc d;
+            std::vector<int64_t> pool;
+            if (!build_desc(b, cards, chain_eb == 8 ? 2 : 4, d, pool, nullptr)) return -1;
+        }
+        double moved = (double)table_size(big.vars, cards);
+        for (size_t i = 1; i < b.in.size(); ++i) {
+            const int j = prod_of[i - 1];
+            if (j >= 0) {
+                const std::vector<View> &sm = steps[j].smalls;
+                std::vector<int64_t> key;
+                for (const View &v : sm) {
+                    key.push_back(v.table);
+                    key.push_back(v.base);
+                    key.insert(key.end(), v.vars.begin(), v.vars.end());
+                    key.push_back(-1);
+                }
+                auto it = gcache.find(key);
+                int t = it != gcache.end() ? it->second : push_bucket(sm, -1, canon(chain_scope(sm)), true);
+                gcache[key] = t;
+                b.in[i] = view(t);
+            }
+            moved += (double)table_size(b.in[i].vars, cards);
+        }
+        b.out_table = new_msg(b.out_vars);
+        int lv = sequential ? last_level : 0;
+        for (const View &v : b.in) lv = std::max(lv, level[v.table]);
+        b.level = lv + 1;
+        last_level = std::max(last_level, b.level);
+        level[b.out_table] = b.level;
+        const double rest = (double)table_size(b.out_vars, cards) / std::pow((double)cards[xs[0]], F);
+        p.entries += F * rest * std::pow((double)cards[xs[0]], F + 1);
+        p.elems_moved += moved + (double)p.msgs[b.out_table - p.n_src].size;
+        p.width = std::max(p.width, (int)b.out_vars.size());
+        p.buckets.push_back(b);
+        return b.out_table;
     }
     // first bucket (by elimination rank >= from) whose variable is in `vars`
     int first_bucket(const std::vector<int> &vars, int from) const {
@@ -655,6 +897,8 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
 
 // ------------------------------------------- chain bucket tree, checkpointed
 namespace {
+constexpr int kChainRunMax = 4;                   // longest fused run tried (fp32, K = 2)
+
 int64_t binom_capped(int n, int k) {             // C(n, k), saturating at 2^40
     if (k < 0 || k > n) return 0;
     k = std::min(k, n - k);
@@ -669,7 +913,7 @@ int64_t binom_capped(int n, int k) {             // C(n, k), saturating at 2^40
 
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
-                            int part, int n_parts, VEPlan &out, std::string *msg) {
+                            int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb) {
     if (n_parts < 1 || part < 0 || part >= n_parts) {
         if (msg) *msg = "bad part";
         return false;
@@ -677,6 +921,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
     VEPlan p;
     PlanBuilder B(cards, p, sources, order, true);
     B.sequential = true;
+    B.chain_eb = chain_eb;
     const int nord = (int)order.size();
     // symbolic forward pass: bucket contents, message scopes, tree shape
     std::vector<std::vector<View>> src_in(nord);
@@ -824,7 +1069,40 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             have_pi = true;
         };
         auto pi_down_to = [&](int j) {
-            for (int jj = pi_pos - 1; jj >= j; --jj) pi_step(jj);
+            int jj = pi_pos - 1;
+            while (jj >= j) {
+                // longest fusable run of backward buckets jj, jj-1, ... (chain.cuh)
+                int fused = 0;
+                for (int F = std::min(kChainRunMax, jj - j + 1); F >= 2 && have_pi && !fused; --F) {
+                    std::vector<PlanBuilder::ChainStep> steps;
+                    std::vector<int> vars = pi_cur.vars;
+                    for (int i = 0; i < F; ++i) {
+                        const std::vector<int> &sep = lam_vars[path[jj - i]];
+                        const std::vector<View> &sm = src_in[path[jj - i + 1]];
+                        std::vector<int> u = vars, y;
+                        for (const View &v : sm)
+                            for (int w : v.vars)
+                                if (!contains(u, w)) u.push_back(w);
+                        for (int w : u)
+                            if (!contains(sep, w)) y.push_back(w);
+                        if (y.size() != 1) break;
+                        steps.push_back({sm, y[0]});
+                        vars = sep;
+                    }
+                    if ((int)steps.size() != F) continue;
+                    const int t = B.emit_chain(pi_cur, steps);
+                    if (t >= 0) {
+                        pi_cur = B.view(t);
+                        fused = F;
+                    }
+                }
+                if (fused) {
+                    jj -= fused;
+                } else {
+                    pi_step(jj);
+                    --jj;
+                }
+            }
             pi_pos = std::min(pi_pos, j);
         };
         int next_deliver = (int)D.size() - 1;
@@ -856,7 +1134,26 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         // lam at position `to` from lam at `from` (-1: from the path's start), streamed
         auto advance = [&](const View *start, int from, int to) {
             View cur = forward(path[from + 1], start);
-            for (int k = from + 2; k <= to; ++k) cur = forward(path[k], &cur);
+            int k = from + 2;
+            while (k <= to) {
+                // longest fusable run of forward buckets k, k+1, ... (chain.cuh)
+                int fused = 0;
+                for (int F = std::min(kChainRunMax, to - k + 1); F >= 2 && !fused; --F) {
+                    std::vector<PlanBuilder::ChainStep> steps;
+                    for (int i = 0; i < F; ++i) steps.push_back({src_in[path[k + i]], order[path[k + i]]});
+                    const int t = B.emit_chain(cur, steps);
+                    if (t >= 0) {
+                        cur = B.view(t);
+                        fused = F;
+                    }
+                }
+                if (fused) {
+                    k += fused;
+                } else {
+                    cur = forward(path[k], &cur);
+                    ++k;
+                }
+            }
             return cur;
         };
         // reverse(lo, hi, start, spos, s): deliver D[hi-1] ... D[lo] (binomial
@@ -1093,7 +1390,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         b.out_table = remap(it.plan, b.out_table);
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
-        it.key = it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2) : variant_key(it.d.n_in, it.d.v1, it.d.v2);
+        it.key = it.d.chain ? chain_key(it.d.chain >> 16, it.d.k, it.d.chain & 0xff)
+                 : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2) : variant_key(it.d.n_in, it.d.v1, it.d.v2);
     });
     for (const Item &it : items)
         if (!it.ok) {
@@ -1121,7 +1419,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
             s.pool.insert(s.pool.end(), it.pool.begin(), it.pool.end());
             d.vblk_begin = vb;
             vb += (d.n_tiles + kBlock - 1) / kBlock;
-            g.small_elems = std::max(g.small_elems, d.big >= 0 ? d.small_elems : 0);
+            g.small_elems = std::max(g.small_elems, d.big >= 0 || d.chain ? d.small_elems : 0);
             if (dump) {
                 std::fprintf(stderr, "L%d n_in=%d k=%d tile=%dx%d big=%d bcls=%d tiles=%lld dims:", g.level, d.n_in, d.k,
                              d.v1, d.v2, d.big, d.big >= 0 ? d.bcls : 0, (long long)d.n_tiles);

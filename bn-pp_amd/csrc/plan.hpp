@@ -42,12 +42,21 @@ struct BucketSpec {
     std::vector<int> out_vars;      // output layout (slowest first)
     int out_table = -1;
     int level = 0;
+    // chain form (bnpp_device.h, ChainForm): in[0] is the message entering a
+    // run of fused buckets, bucket j sums chain_x[j] and brings in chain_n[j];
+    // in[1..] are the G tables of the buckets whose bit is set in chain_gmask
+    std::vector<int> chain_x, chain_n;
+    int chain_gmask = 0;
 };
 
 // Compile one bucket into a descriptor + dims-pool rows.  max_vec: 4 (fp32) / 2 (fp64).
 // Returns false (with msg) on an invalid shape.
 bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec, BucketDesc &d,
                 std::vector<int64_t> &pool, std::string *msg);
+
+// Fused chain runs: largest K^F register table per element size (kernels
+// instantiated in chain.cuh: fp32 K^F <= 16, fp64 <= 8).
+inline int chain_max_entries(int elem_bytes) { return elem_bytes == 4 ? 16 : 8; }
 
 struct MsgTable {
     std::vector<int> vars;
@@ -104,10 +113,12 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
 // (msg) when the tree is not a chain.  part / n_parts: this part owns the
 // marginals of one contiguous segment of the chain; it streams the forward
 // messages up to the segment, runs the backward messages (which need no
-// forward message) down to it, and checkpoints only inside it.
+// forward message) down to it, and checkpoints only inside it.  chain_eb > 0:
+// runs of consecutive buckets are fused into chain kernels for that element
+// size (bnpp_device.h, ChainForm).
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
-                            int part, int n_parts, VEPlan &out, std::string *msg);
+                            int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb = 0);
 
 // Flattened, level-ordered launch schedule over one or more plans sharing the
 // same sources.  Tables: [0, n_src) sources, then every plan's messages.

@@ -173,3 +173,27 @@ def test_tree_parts_sum_to_whole(ctx, n_parts):
         for t, p in got.items():
             assert _close(p, want[t], 1e-12), (part, t, p, want[t])
     assert sorted(seen) == list(range(m.n_vars))
+
+
+@pytest.mark.parametrize("dtype", [bnpp.F64, bnpp.F32])
+def test_tree_chain_fused_runs_identical_to_unfused(ctx, dtype):
+    """Fused sweep runs (chain.cuh: F buckets per pass, intermediate messages in
+    registers) perform each bucket's arithmetic in the reference's order and
+    differ from the one-bucket-per-launch run only by exact powers of two, so
+    the marginals are bit-identical (fp64 and fp32)."""
+    m = bnpp.Model.from_dict(synth.ising_grid(10, 13, seed=5))
+    col = [r * 13 + c for c in range(13) for r in range(10)]
+    ev = {31: 1, 77: 0}
+    os.environ["BNPP_TREE_SLOTS"] = "3"
+    try:
+        fused, _ = bnpp.marginals_tree(ctx, m, ev, "mf", dtype, order=col)
+        os.environ["BNPP_NO_CHAIN"] = "1"
+        plain, _ = bnpp.marginals_tree(ctx, m, ev, "mf", dtype, order=col)
+    finally:
+        del os.environ["BNPP_TREE_SLOTS"]
+        os.environ.pop("BNPP_NO_CHAIN", None)
+    assert fused == plain
+    want, _ = bnpp.marginals(ctx, m, ev, "mf", bnpp.F64)
+    tol = 1e-12 if dtype == bnpp.F64 else 1e-5
+    for t in range(m.n_vars):
+        assert _close(fused[t], want[t], tol), (t, fused[t], want[t])

@@ -161,6 +161,7 @@ def test_plan_stats_checkpointed_chain():
     col = [r * 10 + c for c in range(10) for r in range(10)]
     full = bnpp.plan_stats(m, 3, {}, "mf", order=col)
     os.environ["BNPP_TREE_SLOTS"] = "2"
+    os.environ["BNPP_NO_CHAIN"] = "1"          # one launch per bucket (fused runs add shared G products)
     try:
         ck = bnpp.plan_stats(m, 3, {}, "mf", order=col)
         with pytest.raises(bnpp.BnppError) as e:     # min-fill on alarm: not a chain
@@ -168,6 +169,7 @@ def test_plan_stats_checkpointed_chain():
         assert e.value.status == bnpp.ERR_UNSUPPORTED
     finally:
         del os.environ["BNPP_TREE_SLOTS"]
+        del os.environ["BNPP_NO_CHAIN"]
     assert ck[0] > full[0]                           # recomputation
     assert ck[2] == ck[3]                            # one bucket per level
     assert ck[1] < full[1]                           # smaller arena
@@ -194,3 +196,23 @@ def test_tree_parts_cover_every_marginal_once(n_parts):
     for part in range(n_parts):
         seen += bnpp.plan_tree_part(a, part, n_parts, ev)[0]
     assert sorted(seen) == list(range(a.n_vars))
+
+
+def test_plan_fused_sweep_cuts_traffic():
+    """The 32x32 Ising bucket tree on a column sweep (width 32, checkpointed
+    chain) with fused sweep runs (chain.cuh) plans the same factor-entries as
+    one bucket per launch but at least 3x less algorithmic HBM traffic."""
+    from bnpp import synth
+    m = bnpp.Model.from_dict(synth.ising_grid(32, 32, seed=0))
+    col = [r * 32 + c for c in range(32) for r in range(32)]
+    os.environ["BNPP_MEM_BUDGET_GB"] = "245"
+    try:
+        fused = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+        os.environ["BNPP_NO_CHAIN"] = "1"
+        plain = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+    finally:
+        del os.environ["BNPP_MEM_BUDGET_GB"]
+        os.environ.pop("BNPP_NO_CHAIN", None)
+    assert fused[4] == plain[4] == 32
+    assert abs(fused[0] - plain[0]) < 0.01 * plain[0]
+    assert fused[6] * 3 < plain[6]

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../bn-pp_amd"
 name=$1; flags=$2
 make -s lib/libbnpp.so
 mkdir -p build_$name lib_$name
-for f in launch k_generic_f32 k_generic_f64 k_stream_f32 k_stream_f64; do
+for f in launch k_generic_f32 k_generic_f64 k_stream_f32 k_stream_f64 k_chain_f32 k_chain_f64; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Icsrc -I../include $flags \
       -c csrc/$f.hip -o build_$name/$f.o &
 done
