@@ -347,10 +347,15 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, memory_budget(ctx),
                             batches, job->stats, part, n_parts);
     if (rc) return rc;
+    const double t0 = now_ms();
     rc = upload_sources(ctx->c, d.values, dtype == BNPP_F32 ? kF32 : kF64, job->src);
     if (rc) return from_ctx(ctx, rc);
+    const double t1 = now_ms();
     rc = make_program(ctx->c, job->src, std::move(batches), job->pg);
     if (rc) return from_ctx(ctx, rc);
+    if (std::getenv("BNPP_TIMING"))
+        std::fprintf(stderr, "[bnpp] job: upload %.1f ms, program (arena %.2f GB) %.1f ms\n", t1 - t0,
+                     job->pg.arena_bytes / 1e9, now_ms() - t1);
     return BNPP_OK;
 }
 
@@ -871,12 +876,19 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
     BNPP_GUARD_BEGIN
     if (!out) return set_err(BNPP_ERR_INVALID, "null output");
     double t0 = now_ms();
+    const bool timing = std::getenv("BNPP_TIMING") != nullptr;
     std::unique_ptr<bnpp_job> job;
     int rc = create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job,
                         part, n_parts);
+    const double t1 = now_ms();
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
+    const double t2 = now_ms();
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr, owned);
+    const double t3 = now_ms();
     if (job) destroy_job(job.release());
+    if (timing)
+        std::fprintf(stderr, "[bnpp] tree marginals: create %.1f ms, launch %.1f ms, run+fetch %.1f ms, free %.1f ms\n",
+                     t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
     if (rc) return rc;
     if (uptime_ms) *uptime_ms = now_ms() - t0;
     return BNPP_OK;

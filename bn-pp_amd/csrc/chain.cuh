@@ -91,8 +91,8 @@ __device__ __forceinline__ void chain_load_state(ChainState<F> &c, const BucketD
         c.glds[j] = on ? d.in_lds_off[gi] : 0;
         gi += on ? 1 : 0;
     }
-    c.big = meta[d.in_table[0]].ptr;
-    c.out = meta[d.out_table].ptr;
+    c.big = gptr(meta[d.in_table[0]].ptr);
+    c.out = gptr(meta[d.out_table].ptr);
     int64_t e_sum = 0, x_sum = 0;
     for (int i = 0; i < kMaxIn; ++i) {
         if (i >= d.n_in) break;
@@ -126,11 +126,67 @@ __device__ __forceinline__ void chain_stage(const BucketDesc &d, TableMeta *meta
     __syncthreads();
     for (int i = 1; i < kMaxIn; ++i) {
         if (i >= d.n_in) break;
-        const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
+        const T *src = static_cast<const T *>(gptr(meta[d.in_table[i]].ptr)) + d.in_base[i];
         const int off = d.in_lds_off[i], span = d.in_span[i];
-        for (int e = threadIdx.x; e < span; e += kBlock) small[off + e] = src[e];
+        for (int e = threadIdx.x; e < span; e += kBlock) small[off + e] = gload(src + e);
     }
     __syncthreads();
+}
+
+// Bucket J of a run on the register table t (MODE 0: no factor tables,
+// 1: G_J shared by the thread's V rest entries, 2: G_J varies along them).
+// Every G value the bucket needs is fetched from LDS before any is used (one
+// wait), then each output entry is  acc = 0; acc += G * m  over x_J = 0..K-1.
+template <typename T, int K, int F, int V, int J, int MODE>
+__device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small, int32_t gb, int32_t gv,
+                                           const int32_t (&gs)[F], int32_t gsn) {
+    using S = ChainShape<K, F>;
+    constexpr int N = S::N;
+    constexpr int PJ = S::place(J);
+    constexpr int NA = N / K;                       // assignments of the other slots
+    constexpr int NG = MODE == 2 ? V : 1;
+    T g[MODE == 0 ? 1 : NA][K][K][NG];
+    if constexpr (MODE != 0) {
+        static_for<NA>([&](auto ic) {
+            constexpr int ai = decltype(ic)::value;
+            constexpr int a = (ai / PJ) * PJ * K + ai % PJ;          // slot J digit 0
+            int32_t go = gb;
+#pragma unroll
+            for (int p = 0; p < F; ++p)
+                if (p != J) go += S::digit(a, p) * gs[p];
+#pragma unroll
+            for (int n = 0; n < K; ++n)
+#pragma unroll
+                for (int x = 0; x < K; ++x)
+#pragma unroll
+                    for (int v = 0; v < NG; ++v) g[ai][n][x][v] = small[go + x * gs[J] + n * gsn + v * gv];
+        });
+    }
+    static_for<NA>([&](auto ic) {
+        constexpr int ai = decltype(ic)::value;
+        constexpr int a = (ai / PJ) * PJ * K + ai % PJ;
+        T nw[K][V];
+#pragma unroll
+        for (int n = 0; n < K; ++n) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) nw[n][v] = T(0);
+#pragma unroll
+            for (int x = 0; x < K; ++x) {
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const T m = t[a + x * PJ][v];
+                    T p = m;
+                    if constexpr (MODE == 1) p = g[ai][n][x][0] * m;
+                    if constexpr (MODE == 2) p = g[ai][n][x][v] * m;
+                    nw[n][v] = nw[n][v] + p;
+                }
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < K; ++n)
+#pragma unroll
+            for (int v = 0; v < V; ++v) t[a + n * PJ][v] = nw[n][v];
+    });
 }
 
 template <typename T, int K, int F, int FORM>
@@ -203,14 +259,14 @@ __global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *_
                     int64_t o = in_off;
 #pragma unroll
                     for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.is[p];
-                    t[a][0] = big[o];
+                    t[a][0] = gload(big + o);
                 }
             } else {
                 // K^F contiguous entries (slot 0 fastest) per rest entry
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                     T buf[N];
-                    load_n<T, N, kNtLoad>(big + in_off + v * in_v, buf);
+                    load_n<T, N, kNtLoad, true>(big + in_off + v * in_v, buf);
 #pragma unroll
                     for (int a = 0; a < N; ++a) t[a][v] = buf[S::rev(a)];
                 }
@@ -218,35 +274,10 @@ __global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *_
             // the F buckets of the run, in order
             static_for<F>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                const bool has_g = (c.gmask >> j) & 1;           // uniform
-                static_for<N>([&](auto ac) {
-                    constexpr int a = decltype(ac)::value;
-                    if constexpr (S::digit(a, j) == 0) {
-                        int32_t go = gb[j];
-#pragma unroll
-                        for (int p = 0; p < F; ++p)
-                            if (p != j) go += S::digit(a, p) * c.gs[j][p];
-                        T nw[K][V];
-#pragma unroll
-                        for (int n = 0; n < K; ++n) {
-#pragma unroll
-                            for (int v = 0; v < V; ++v) nw[n][v] = T(0);
-#pragma unroll
-                            for (int x = 0; x < K; ++x) {
-#pragma unroll
-                                for (int v = 0; v < V; ++v) {
-                                    const T m = t[a + x * S::place(j)][v];
-                                    const T p = has_g ? small[go + x * c.gs[j][j] + n * c.gsn[j] + v * gv[j]] * m : m;
-                                    nw[n][v] = nw[n][v] + p;
-                                }
-                            }
-                        }
-#pragma unroll
-                        for (int n = 0; n < K; ++n)
-#pragma unroll
-                            for (int v = 0; v < V; ++v) t[a + n * S::place(j)][v] = nw[n][v];
-                    }
-                });
+                if (!((c.gmask >> j) & 1))
+                    chain_step<T, K, F, V, j, 0>(t, small, gb[j], gv[j], c.gs[j], c.gsn[j]);
+                else                       // V > 1: G_j constant along the V entries (planner-checked)
+                    chain_step<T, K, F, V, j, 1>(t, small, gb[j], gv[j], c.gs[j], c.gsn[j]);
             });
             if (c.flags & kScale) {
 #pragma unroll
@@ -265,7 +296,7 @@ __global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *_
                     int64_t o = out_off;
 #pragma unroll
                     for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.os[p];
-                    store_n<T, V, kNtStore>(out + o, t[a]);
+                    store_n<T, V, kNtStore, true>(out + o, t[a]);
                 }
             }
         }

@@ -52,51 +52,87 @@ template <> struct FBits<double> {
 template <typename T, int W>
 using vec_t = T __attribute__((ext_vector_type(W)));
 
-template <int W, bool NT, typename T>
-__device__ __forceinline__ vec_t<T, W> vload(const T *p) {
-    const vec_t<T, W> *q = reinterpret_cast<const vec_t<T, W> *>(p);
-    if constexpr (NT) return __builtin_nontemporal_load(q);
-    else return *q;
-}
-template <int W, bool NT, typename T>
-__device__ __forceinline__ void vstore(T *p, vec_t<T, W> v) {
-    vec_t<T, W> *q = reinterpret_cast<vec_t<T, W> *>(p);
-    if constexpr (NT) __builtin_nontemporal_store(v, q);
-    else *q = v;
-}
+// G: the pointer is into device memory (a table).  Table pointers come out of
+// TableMeta as generic pointers, and accesses through them would compile to
+// flat_* instructions, which also count against lgkmcnt (so every LDS wait
+// would stall on the HBM loads in flight); the cast at the access makes them
+// global_* instructions.
+template <typename T>
+using gbl_t = __attribute__((address_space(1))) T;
 
-template <typename T, int N, bool NT = false>
+template <int W, bool NT, bool G = false, typename T>
+__device__ __forceinline__ vec_t<T, W> vload(const T *p) {
+    if constexpr (G) {
+        const gbl_t<vec_t<T, W>> *q = (const gbl_t<vec_t<T, W>> *)p;
+        if constexpr (NT) return __builtin_nontemporal_load(q);
+        else return *q;
+    } else {
+        const vec_t<T, W> *q = reinterpret_cast<const vec_t<T, W> *>(p);
+        if constexpr (NT) return __builtin_nontemporal_load(q);
+        else return *q;
+    }
+}
+template <int W, bool NT, bool G = false, typename T>
+__device__ __forceinline__ void vstore(T *p, vec_t<T, W> v) {
+    if constexpr (G) {
+        gbl_t<vec_t<T, W>> *q = (gbl_t<vec_t<T, W>> *)p;
+        if constexpr (NT) __builtin_nontemporal_store(v, q);
+        else *q = v;
+    } else {
+        vec_t<T, W> *q = reinterpret_cast<vec_t<T, W> *>(p);
+        if constexpr (NT) __builtin_nontemporal_store(v, q);
+        else *q = v;
+    }
+}
+// one element of a table in device memory
+template <typename T>
+__device__ __forceinline__ T gload(const T *p) { return *(const gbl_t<T> *)p; }
+
+template <typename T, int N, bool NT = false, bool G = false>
 __device__ __forceinline__ void load_n(const T *p, T *x) {
     constexpr int W = (sizeof(T) == 4 && N % 4 == 0) ? 4 : (N % 2 == 0 ? 2 : 1);
     if constexpr (W == 1) {
 #pragma unroll
-        for (int c = 0; c < N; ++c) x[c] = NT ? __builtin_nontemporal_load(p + c) : p[c];
+        for (int c = 0; c < N; ++c) {
+            if constexpr (G) {
+                const gbl_t<T> *q = (const gbl_t<T> *)(p + c);
+                x[c] = NT ? __builtin_nontemporal_load(q) : *q;
+            } else {
+                x[c] = NT ? __builtin_nontemporal_load(p + c) : p[c];
+            }
+        }
     } else {
 #pragma unroll
         for (int c = 0; c < N / W; ++c) {
-            vec_t<T, W> v = vload<W, NT>(p + W * c);
+            vec_t<T, W> v = vload<W, NT, G>(p + W * c);
 #pragma unroll
             for (int e = 0; e < W; ++e) x[W * c + e] = v[e];
         }
     }
 }
-template <typename T, int N, bool NT = false>
+template <typename T, int N, bool NT = false, bool G = false>
 __device__ __forceinline__ void store_n(T *p, const T *x) {
     constexpr int W = (sizeof(T) == 4 && N % 4 == 0) ? 4 : (N % 2 == 0 ? 2 : 1);
     if constexpr (W == 1) {
 #pragma unroll
         for (int c = 0; c < N; ++c) {
-            if constexpr (NT) __builtin_nontemporal_store(x[c], p + c);
-            else p[c] = x[c];
+            if constexpr (G) {
+                gbl_t<T> *q = (gbl_t<T> *)(p + c);
+                if constexpr (NT) __builtin_nontemporal_store(x[c], q);
+                else *q = x[c];
+            } else {
+                if constexpr (NT) __builtin_nontemporal_store(x[c], p + c);
+                else p[c] = x[c];
+            }
         }
-    } else {
+        return;
+    }
 #pragma unroll
-        for (int c = 0; c < N / W; ++c) {
-            vec_t<T, W> v;
+    for (int c = 0; c < N / W; ++c) {
+        vec_t<T, W> v;
 #pragma unroll
-            for (int e = 0; e < W; ++e) v[e] = x[W * c + e];
-            vstore<W, NT>(p + W * c, v);
-        }
+        for (int e = 0; e < W; ++e) v[e] = x[W * c + e];
+        vstore<W, NT, G>(p + W * c, v);
     }
 }
 
@@ -108,6 +144,15 @@ __device__ __forceinline__ void store_n(T *p, const T *x) {
 #endif
 constexpr bool kNtLoad = BNPP_NT_LOAD != 0;
 constexpr bool kNtStore = BNPP_NT_STORE != 0;
+
+// A table pointer read from TableMeta is a generic pointer: accesses through
+// it compile to flat_* instructions, which also count against lgkmcnt, so
+// every LDS wait would stall on the HBM loads in flight.  Tables live in
+// device memory: assert the global address space (global_* instructions).
+template <typename P>
+__device__ __forceinline__ P *gptr(P *p) {
+    return (P *)(__attribute__((address_space(1))) P *)p;
+}
 
 __device__ __forceinline__ double ldexp_t(double x, int e) { return __builtin_amdgcn_ldexp(x, e); }
 __device__ __forceinline__ float ldexp_t(float x, int e) { return __builtin_amdgcn_ldexpf(x, e); }
@@ -287,7 +332,7 @@ __device__ __forceinline__ void store_tiles(T *out, int64_t wave_tid0, int64_t n
     const int64_t tid = wave_tid0 + lane;
     constexpr int row_bytes = TS * (int)sizeof(T);
     if constexpr (row_bytes <= 16 || BNPP_DIRECT_STORE != 0) {
-        if (tid < n_tiles) store_n<T, TS, kNtStore>(out + tid * TS, acc);
+        if (tid < n_tiles) store_n<T, TS, kNtStore, true>(out + tid * TS, acc);
     } else {
         constexpr int rowp = row_bytes + kLdsRowPad;
         constexpr int cpr = row_bytes / 16;                   // 16-B chunks per row
@@ -303,7 +348,7 @@ __device__ __forceinline__ void store_tiles(T *out, int64_t wave_tid0, int64_t n
             if (src_lane < valid) {
                 T x[EPC];
                 load_n<T, EPC>(reinterpret_cast<const T *>(lds + src_lane * rowp + within * 16), x);
-                store_n<T, EPC, kNtStore>(out + wave_tid0 * TS + (int64_t)q * EPC, x);
+                store_n<T, EPC, kNtStore, true>(out + wave_tid0 * TS + (int64_t)q * EPC, x);
             }
         }
     }
@@ -380,12 +425,12 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
             cur_begin = d.vblk_begin;
             load_common(b, d, pool + d.dim_off);
             b.flags = d.flags;
-            b.out = meta[d.out_table].ptr;
+            b.out = gptr(meta[d.out_table].ptr);
             int64_t e_sum = 0, x_sum = 0;
             for (int i = 0; i < kMaxIn; ++i) {
                 if (i < d.n_in) {
                     const TableMeta &mi = meta[d.in_table[i]];
-                    b.ptr[i] = mi.ptr;
+                    b.ptr[i] = gptr(mi.ptr);
                     int e = FBits<T>::exponent(mi.maxbits);
                     if (d.flags & kScale) {
                         e_sum += e;
@@ -741,12 +786,12 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_level_ker
             load_common(b, d, pool + d.dim_off);
             load_stream_state(st, d);
             b.flags = d.flags;
-            b.out = meta[d.out_table].ptr;
+            b.out = gptr(meta[d.out_table].ptr);
             int64_t e_sum = 0, x_sum = 0;
             for (int i = 0; i < kMaxIn; ++i) {
                 if (i < d.n_in) {
                     const TableMeta &mi = meta[d.in_table[i]];
-                    b.ptr[i] = mi.ptr;
+                    b.ptr[i] = gptr(mi.ptr);
                     int e = FBits<T>::exponent(mi.maxbits);
                     if (d.flags & kScale) {
                         e_sum += e;

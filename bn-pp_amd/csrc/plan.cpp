@@ -201,6 +201,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         bwd = bwd && !md.empty() && md[0].out == 1 && md[0].card % (uint64_t)bv == 0 && big.base % W == 0;
         for (const RDim &r : md) bwd = bwd && r.in % W == 0 && (r.out % bv == 0 || &r == &md[0]);
         for (int p = 0; bwd && p < F; ++p) bwd = os[p] % bv == 0;
+        for (int j = 0; bwd && j < F; ++j) bwd = md[0].g[j] == 0;      // G constant along a thread's V entries
         if (fwd) form = kChainFwd;
         else if (bwd) { form = kChainBwd; V = bv; }
         else return fail("chain: layout fits no kernel form");
