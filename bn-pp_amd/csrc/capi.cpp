@@ -147,6 +147,8 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
     auto scopes = conditioned_scopes(d, ev);
     auto views = source_views(d, ev);
     max_width = 0;
+    const char *nc = std::getenv("BNPP_NO_CHAIN");                 // A/B: one launch per bucket
+    const int chain_eb = nc && *nc == '1' ? 0 : eb;
     if (heuristic < BNPP_ORDER_GIVEN || heuristic > BNPP_MIN_DEGREE)
         return set_err(BNPP_ERR_INVALID, "unknown heuristic");
     if (kind == 2) {                                     // caller-chosen variables
@@ -172,7 +174,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                 if (ev[v] < 0) vars.push_back(v);        // model.cpp:277-282
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
-        plans.push_back(plan_ve(d.cards, views, ord, true));
+        plans.push_back(plan_ve(d.cards, views, ord, true, chain_eb));
     } else if (kind == 3) {
         // all marginals from one two-pass bucket tree over the PR ordering
         std::vector<int> vars, ord;
@@ -194,8 +196,6 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
         plans.push_back(plan_bucket_tree(d.cards, views, ord, targets, part, n_parts));
-        const char *nc = std::getenv("BNPP_NO_CHAIN");             // A/B: unfused sweeps
-        const int chain_eb = nc && *nc == '1' ? 0 : eb;
         auto need = [&](const VEPlan &p) { return plan_arena_bytes(p, eb) + (int64_t)p.buckets.size() * 512; };
         const char *force = std::getenv("BNPP_TREE_SLOTS");     // testing / tuning: chain mode, fixed slots
         if (force && std::atoi(force) > 0) {

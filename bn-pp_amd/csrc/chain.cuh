@@ -91,8 +91,8 @@ __device__ __forceinline__ void chain_load_state(ChainState<F> &c, const BucketD
         c.glds[j] = on ? d.in_lds_off[gi] : 0;
         gi += on ? 1 : 0;
     }
-    c.big = gptr(meta[d.in_table[0]].ptr);
-    c.out = gptr(meta[d.out_table].ptr);
+    c.big = meta[d.in_table[0]].ptr;
+    c.out = meta[d.out_table].ptr;
     int64_t e_sum = 0, x_sum = 0;
     for (int i = 0; i < kMaxIn; ++i) {
         if (i >= d.n_in) break;
@@ -126,7 +126,7 @@ __device__ __forceinline__ void chain_stage(const BucketDesc &d, TableMeta *meta
     __syncthreads();
     for (int i = 1; i < kMaxIn; ++i) {
         if (i >= d.n_in) break;
-        const T *src = static_cast<const T *>(gptr(meta[d.in_table[i]].ptr)) + d.in_base[i];
+        const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
         const int off = d.in_lds_off[i], span = d.in_span[i];
         for (int e = threadIdx.x; e < span; e += kBlock) small[off + e] = gload(src + e);
     }

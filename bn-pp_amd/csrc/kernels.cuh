@@ -145,15 +145,6 @@ __device__ __forceinline__ void store_n(T *p, const T *x) {
 constexpr bool kNtLoad = BNPP_NT_LOAD != 0;
 constexpr bool kNtStore = BNPP_NT_STORE != 0;
 
-// A table pointer read from TableMeta is a generic pointer: accesses through
-// it compile to flat_* instructions, which also count against lgkmcnt, so
-// every LDS wait would stall on the HBM loads in flight.  Tables live in
-// device memory: assert the global address space (global_* instructions).
-template <typename P>
-__device__ __forceinline__ P *gptr(P *p) {
-    return (P *)(__attribute__((address_space(1))) P *)p;
-}
-
 __device__ __forceinline__ double ldexp_t(double x, int e) { return __builtin_amdgcn_ldexp(x, e); }
 __device__ __forceinline__ float ldexp_t(float x, int e) { return __builtin_amdgcn_ldexpf(x, e); }
 
@@ -197,15 +188,15 @@ __device__ __forceinline__ void load_tile(const T *src, int64_t s0, int64_t s1, 
     constexpr int TS = V1 * V2;
     if (s0 == 0) {
         if (V2 == 1 || s1 == 0) {                         // broadcast over the tile
-            T y = src[0];
+            T y = gload(src);
 #pragma unroll
             for (int j = 0; j < TS; ++j) x[j] = y;
         } else {
             T y[V2];
-            if (s1 == 1) load_n<T, V2>(src, y);
+            if (s1 == 1) load_n<T, V2, false, true>(src, y);
             else {
 #pragma unroll
-                for (int j2 = 0; j2 < V2; ++j2) y[j2] = src[(int64_t)j2 * s1];
+                for (int j2 = 0; j2 < V2; ++j2) y[j2] = gload(src + (int64_t)j2 * s1);
             }
 #pragma unroll
             for (int j2 = 0; j2 < V2; ++j2)
@@ -215,20 +206,20 @@ __device__ __forceinline__ void load_tile(const T *src, int64_t s0, int64_t s1, 
     } else if (V1 > 1 && s0 == 1) {                       // contiguous along the fastest dim
         if (V2 == 1 || s1 == 0) {
             T y[V1];
-            load_n<T, V1>(src, y);
+            load_n<T, V1, false, true>(src, y);
 #pragma unroll
             for (int j2 = 0; j2 < V2; ++j2)
 #pragma unroll
                 for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = y[j1];
         } else {
 #pragma unroll
-            for (int j2 = 0; j2 < V2; ++j2) load_n<T, V1>(src + (int64_t)j2 * s1, x + j2 * V1);
+            for (int j2 = 0; j2 < V2; ++j2) load_n<T, V1, false, true>(src + (int64_t)j2 * s1, x + j2 * V1);
         }
     } else {                                              // general gather
 #pragma unroll
         for (int j2 = 0; j2 < V2; ++j2)
 #pragma unroll
-            for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = src[(int64_t)j1 * s0 + (int64_t)j2 * s1];
+            for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = gload(src + (int64_t)j1 * s0 + (int64_t)j2 * s1);
     }
 }
 
@@ -425,12 +416,12 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
             cur_begin = d.vblk_begin;
             load_common(b, d, pool + d.dim_off);
             b.flags = d.flags;
-            b.out = gptr(meta[d.out_table].ptr);
+            b.out = meta[d.out_table].ptr;
             int64_t e_sum = 0, x_sum = 0;
             for (int i = 0; i < kMaxIn; ++i) {
                 if (i < d.n_in) {
                     const TableMeta &mi = meta[d.in_table[i]];
-                    b.ptr[i] = gptr(mi.ptr);
+                    b.ptr[i] = mi.ptr;
                     int e = FBits<T>::exponent(mi.maxbits);
                     if (d.flags & kScale) {
                         e_sum += e;
@@ -501,18 +492,18 @@ struct BigTile {
     static constexpr int N = BC == kBigRow ? V1 : BC == kBigCol ? V2 : (BC == kBigOne || BC >= kBigInter2) ? 1 : TS;
     static __device__ __forceinline__ void issue(const T *src, int64_t s0, int64_t s1, T (&buf)[N]) {
         if constexpr (BC == kBigOne) {
-            buf[0] = src[0];
+            buf[0] = gload(src);
         } else if constexpr (BC == kBigRow) {
-            load_n<T, V1, kNtLoad>(src, buf);
+            load_n<T, V1, kNtLoad, true>(src, buf);
         } else if constexpr (BC == kBigCol) {
-            load_n<T, V2, kNtLoad>(src, buf);
+            load_n<T, V2, kNtLoad, true>(src, buf);
         } else if constexpr (BC == kBigFull) {
-            load_n<T, TS, kNtLoad>(src, buf);
+            load_n<T, TS, kNtLoad, true>(src, buf);
         } else {
 #pragma unroll
             for (int j2 = 0; j2 < V2; ++j2)
 #pragma unroll
-                for (int j1 = 0; j1 < V1; ++j1) buf[j2 * V1 + j1] = src[(int64_t)j1 * s0 + (int64_t)j2 * s1];
+                for (int j1 = 0; j1 < V1; ++j1) buf[j2 * V1 + j1] = gload(src + (int64_t)j1 * s0 + (int64_t)j2 * s1);
         }
     }
     static __device__ __forceinline__ void apply(const T (&buf)[N], T (&p)[TS]) {
@@ -635,7 +626,7 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
         // contiguous values, fetched by one vector load (V2 == 1)
         constexpr int K = BC == kBigInter2 ? 2 : 4;
         T all[V1 * K];
-        load_n<T, V1 * K, kNtLoad>(bsrc, all);
+        load_n<T, V1 * K, kNtLoad, true>(bsrc, all);
 #pragma unroll
         for (int v = 0; v < K; ++v) {
             T p[TS];
@@ -727,7 +718,7 @@ __device__ __forceinline__ void stream_store(const LoadedBucket &b, int64_t tid0
             const int64_t os1 = b.dims[(int64_t)b.n_dims * (2 + b.n_in) + 1];
             T *o = static_cast<T *>(b.out) + out_off;
 #pragma unroll
-            for (int j2 = 0; j2 < V2; ++j2) store_n<T, V1, kNtStore>(o + j2 * os1, acc + j2 * V1);
+            for (int j2 = 0; j2 < V2; ++j2) store_n<T, V1, kNtStore, true>(o + j2 * os1, acc + j2 * V1);
         }
     } else {
         store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
@@ -744,7 +735,7 @@ __device__ __forceinline__ void stage_small(const LoadedBucket &b, const StreamS
         if (i >= b.n_in) break;
         if (i == st.big) continue;
         const T *src = static_cast<const T *>(b.ptr[i]) + b.base[i];
-        for (int e = threadIdx.x; e < st.span[i]; e += kBlock) small[st.lds_off[i] + e] = src[e];
+        for (int e = threadIdx.x; e < st.span[i]; e += kBlock) small[st.lds_off[i] + e] = gload(src + e);
     }
     __syncthreads();
 }
@@ -786,12 +777,12 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_level_ker
             load_common(b, d, pool + d.dim_off);
             load_stream_state(st, d);
             b.flags = d.flags;
-            b.out = gptr(meta[d.out_table].ptr);
+            b.out = meta[d.out_table].ptr;
             int64_t e_sum = 0, x_sum = 0;
             for (int i = 0; i < kMaxIn; ++i) {
                 if (i < d.n_in) {
                     const TableMeta &mi = meta[d.in_table[i]];
-                    b.ptr[i] = gptr(mi.ptr);
+                    b.ptr[i] = mi.ptr;
                     int e = FBits<T>::exponent(mi.maxbits);
                     if (d.flags & kScale) {
                         e_sum += e;

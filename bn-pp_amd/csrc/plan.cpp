@@ -516,6 +516,8 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
 }
 
 // ---------------------------------------------------------------- VE plan
+constexpr int kChainRunMax = 4;                   // longest fused run tried (fp32, K = 2)
+
 namespace {
 // Emits buckets and message tables into a VEPlan (shared by plan_ve and
 // plan_bucket_tree).  Levels: a bucket runs one level after its latest input.
@@ -784,10 +786,12 @@ struct PlanBuilder {
 }  // namespace
 
 VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, const std::vector<int> &order,
-               bool canonical) {
+               bool canonical, int chain_eb) {
     VEPlan p;
     PlanBuilder B(cards, p, sources, order, canonical);
+    B.chain_eb = canonical ? chain_eb : 0;
     const int nord = (int)order.size();
+    auto is_msg = [&](const View &v) { return v.table >= p.n_src; };
     std::vector<std::vector<View>> buckets(nord);
     std::vector<View> result;
     for (const View &s : sources) {                                   // model.cpp:394-406
@@ -797,6 +801,43 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
     }
     for (int i = 0; i < nord; ++i) {                                  // model.cpp:409-439
         if (buckets[i].empty()) continue;   // Factor(1.0).sum_out(x) == 1: result *= 1 is exact
+        // a sweep: bucket i holds factor tables and ONE message (last in its
+        // chain), its message goes to bucket i+1, which holds only factor
+        // tables, and so on -> one fused run (chain.cuh), same arithmetic
+        int fused = 0;
+        if (B.chain_eb && is_msg(buckets[i].back())) {
+            int n_msg = 0;
+            for (const View &v : buckets[i]) n_msg += is_msg(v);
+            for (int F = std::min(kChainRunMax, nord - i); F >= 2 && n_msg == 1 && !fused; --F) {
+                const View big = buckets[i].back();
+                std::vector<PlanBuilder::ChainStep> steps;
+                std::vector<int> vars = big.vars;
+                bool ok = true;
+                for (int k = 0; k < F && ok; ++k) {
+                    std::vector<View> sm = buckets[i + k];
+                    if (k == 0) sm.pop_back();
+                    for (const View &v : sm) ok = ok && !is_msg(v);
+                    if (k > 0) ok = ok && !sm.empty() && B.first_bucket(vars, i + k) == i + k;
+                    for (const View &v : sm)
+                        for (int w : v.vars)
+                            if (!contains(vars, w)) vars.push_back(w);
+                    vars = remove_var(vars, order[i + k]);
+                    steps.push_back({sm, order[i + k]});
+                }
+                if (!ok) continue;
+                const int t = B.emit_chain(big, steps);
+                if (t < 0) continue;
+                View mv = B.view(t);
+                int bi = B.first_bucket(mv.vars, i + F);
+                if (bi >= 0) buckets[bi].push_back(mv);
+                else result.push_back(mv);
+                fused = F;
+            }
+        }
+        if (fused) {
+            i += fused - 1;
+            continue;
+        }
         int t = B.emit(buckets[i], order[i], false);
         View mv = B.view(t);
         int bi = B.first_bucket(mv.vars, i + 1);
@@ -898,8 +939,6 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
 
 // ------------------------------------------- chain bucket tree, checkpointed
 namespace {
-constexpr int kChainRunMax = 4;                   // longest fused run tried (fp32, K = 2)
-
 int64_t binom_capped(int n, int k) {             // C(n, k), saturating at 2^40
     if (k < 0 || k > n) return 0;
     k = std::min(k, n - k);

@@ -91,7 +91,7 @@ struct VEPlan {
 // kMaxIn inputs are split into materialised pure-product prefixes exactly like
 // the reference's left-to-right chain.
 VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, const std::vector<int> &order,
-               bool canonical);
+               bool canonical, int chain_eb = 0);
 
 // All marginals of `targets` from one two-pass bucket tree over `order`
 // (Shafer-Shenoy on the VE bucket tree; replaces the N independent VEs of
