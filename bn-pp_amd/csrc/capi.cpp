@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -24,6 +25,7 @@ using namespace bnpp;
 
 struct bnpp_ctx {
     Context c;
+    std::mutex cache_mu;            // one one-shot call at a time uses c.arena_cache
 };
 struct bnpp_model {
     ModelData d;
@@ -315,14 +317,15 @@ int64_t memory_budget(bnpp_ctx *ctx) {
     if (ctx) {
         size_t fr = 0, tot = 0;
         (void)hipSetDevice(ctx->c.device);
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) return (int64_t)(fr * 0.85);
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0)
+            return (int64_t)((fr + ctx->c.arena_cache_bytes) * 0.85);   // the cached arena is reusable
     }
     return (int64_t)64e9;
 }
 
 int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals,
                int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
-               std::unique_ptr<bnpp_job> &job, int part = 0, int n_parts = 1) {
+               std::unique_ptr<bnpp_job> &job, int part = 0, int n_parts = 1, bool use_cache = false) {
     if (!ctx || !m) return set_err(BNPP_ERR_INVALID, "null context or model");
     if (dtype != BNPP_F32 && dtype != BNPP_F64) return set_err(BNPP_ERR_INVALID, "bad dtype");
     const ModelData &d = m->d;
@@ -351,7 +354,7 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     rc = upload_sources(ctx->c, d.values, dtype == BNPP_F32 ? kF32 : kF64, job->src);
     if (rc) return from_ctx(ctx, rc);
     const double t1 = now_ms();
-    rc = make_program(ctx->c, job->src, std::move(batches), job->pg);
+    rc = make_program(ctx->c, job->src, std::move(batches), job->pg, use_cache);
     if (rc) return from_ctx(ctx, rc);
     if (std::getenv("BNPP_TIMING"))
         std::fprintf(stderr, "[bnpp] job: upload %.1f ms, program (arena %.2f GB) %.1f ms\n", t1 - t0,
@@ -465,6 +468,7 @@ int bnpp_ctx_destroy(bnpp_ctx *ctx) {
     if (!ctx) return BNPP_OK;
     (void)hipSetDevice(ctx->c.device);
     if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
+    drop_arena_cache(ctx->c);
     delete ctx;
     return BNPP_OK;
 }
@@ -737,7 +741,10 @@ int bnpp_variable_elimination(bnpp_ctx *ctx, const bnpp_model *m, int n_vars, co
     BNPP_GUARD_BEGIN
     if (!out_ndims || !out_size || !exp2 || (n_vars > 0 && !vars)) return set_err(BNPP_ERR_INVALID, "null argument");
     std::unique_ptr<bnpp_job> job;
-    int rc = create_job(ctx, m, 2, 0, nullptr, nullptr, heuristic, vars, n_vars, 0, nullptr, dtype, job);
+    std::unique_lock<std::mutex> lk;
+    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
+    int rc = create_job(ctx, m, 2, 0, nullptr, nullptr, heuristic, vars, n_vars, 0, nullptr, dtype, job, 0, 1,
+                        lk.owns_lock());
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     std::vector<std::vector<double>> vals;
     std::vector<int64_t> e2;
@@ -834,7 +841,10 @@ int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     BNPP_GUARD_BEGIN
     double t0 = now_ms();
     std::unique_ptr<bnpp_job> job;
-    int rc = create_job(ctx, m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype, job);
+    std::unique_lock<std::mutex> lk;
+    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
+    int rc = create_job(ctx, m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype, job, 0, 1,
+                        lk.owns_lock());
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     double lz = 0, zz = 0;
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, &lz, &zz);
@@ -853,7 +863,10 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     if (!out) return set_err(BNPP_ERR_INVALID, "null output");
     double t0 = now_ms();
     std::unique_ptr<bnpp_job> job;
-    int rc = create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, job);
+    std::unique_lock<std::mutex> lk;
+    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
+    int rc = create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, job, 0, 1,
+                        lk.owns_lock());
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
     if (job) destroy_job(job.release());
@@ -878,8 +891,10 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
     double t0 = now_ms();
     const bool timing = std::getenv("BNPP_TIMING") != nullptr;
     std::unique_ptr<bnpp_job> job;
+    std::unique_lock<std::mutex> lk;
+    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
     int rc = create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job,
-                        part, n_parts);
+                        part, n_parts, lk.owns_lock());
     const double t1 = now_ms();
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     const double t2 = now_ms();

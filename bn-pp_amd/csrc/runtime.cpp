@@ -180,15 +180,33 @@ void free_executable(Executable &ex) {
     ex = Executable{};
 }
 
-int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg) {
+void drop_arena_cache(Context &ctx) {
+    if (ctx.arena_cache) (void)hipFree(ctx.arena_cache);
+    ctx.arena_cache = nullptr;
+    ctx.arena_cache_bytes = 0;
+}
+
+int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg,
+                 bool use_cache) {
     pg = Program{};
     pg.dtype = src.dtype;
     const int64_t eb = src.dtype == kF32 ? 4 : 8;
     for (const Schedule &s : batches) pg.arena_bytes = std::max(pg.arena_bytes, s.arena_bytes);
     hipError_t err = hipSetDevice(ctx.device);
     if (err != hipSuccess) return fail(ctx, err, "hipSetDevice");
-    if ((err = hipMalloc(&pg.arena, pg.arena_bytes > 0 ? (size_t)pg.arena_bytes : 256)) != hipSuccess)
-        return fail(ctx, err, "hipMalloc(arena)");
+    const int64_t need = std::max<int64_t>(pg.arena_bytes, 256);
+    if (use_cache && ctx.arena_cache && ctx.arena_cache_bytes >= need) {
+        pg.arena = ctx.arena_cache;
+        pg.arena_cached = true;
+    } else {
+        if (use_cache) drop_arena_cache(ctx);            // too small: replace it
+        if ((err = hipMalloc(&pg.arena, (size_t)need)) != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
+        if (use_cache) {
+            ctx.arena_cache = pg.arena;
+            ctx.arena_cache_bytes = need;
+            pg.arena_cached = true;
+        }
+    }
     for (const Schedule &s : batches) {
         std::vector<int64_t> off, sz;
         for (int t : s.plan_result_table) {
@@ -276,7 +294,7 @@ int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std
 
 void free_program(Program &pg) {
     for (Executable &ex : pg.parts) free_executable(ex);
-    if (pg.arena) (void)hipFree(pg.arena);
+    if (pg.arena && !pg.arena_cached) (void)hipFree(pg.arena);
     if (pg.results) (void)hipFree(pg.results);
     pg = Program{};
 }

@@ -32,6 +32,11 @@ struct Context {
     hipStream_t stream = nullptr;
     int max_grid = 2048;
     std::string last_error;
+    // arena kept between one-shot calls (partition / marginals): mapping and
+    // unmapping a few hundred GB of HBM costs ~1 s each way, like a caching
+    // allocator the context holds on to it until it is destroyed
+    void *arena_cache = nullptr;
+    int64_t arena_cache_bytes = 0;
 };
 
 // Sources uploaded for one dtype: one device buffer, each factor pre-scaled by
@@ -64,6 +69,7 @@ struct Program {
     std::vector<Executable> parts;
     void *arena = nullptr;
     int64_t arena_bytes = 0;
+    bool arena_cached = false;          // arena is the context's cache (not freed with the program)
     void *results = nullptr;
     int64_t results_bytes = 0;
     std::vector<std::vector<int64_t>> res_off;    // per part, per plan: byte offset (-1: constant 1)
@@ -79,7 +85,10 @@ int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<
                   std::vector<int64_t> &exp2);
 void free_executable(Executable &ex);
 
-int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg);
+int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg,
+                 bool use_cache = false);
+// release the context's cached arena
+void drop_arena_cache(Context &ctx);
 int launch_program(Context &ctx, Program &pg, hipStream_t stream);
 // result values (as stored, double) and exp2 of every plan, batches in order
 int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std::vector<double>> &vals,
