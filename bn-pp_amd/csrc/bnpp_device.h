@@ -38,6 +38,9 @@ enum BucketFlags : int32_t {
     kTrackMax = 2,     // raise meta[out].maxbits
     kOutStrided = 4,   // dims permuted: output offset from per-dim output strides
                        // (n_dims words after the dims rows in the pool)
+    kChainLo32 = 8,    // chain form: the streamed side (forward input / backward output)
+                       // is linear in the thread index, so one wave's accesses are a
+                       // uniform base + a 32-bit lane offset (saddr addressing)
 };
 
 // Each thread evaluates a V1 x V2 register tile of the output: V1 entries of
@@ -61,7 +64,7 @@ struct BucketDesc {
     int32_t in_lds_off[kMaxIn];     // element offset of each small input in LDS
     int32_t in_span[kMaxIn];        // elements of each small input's reachable range
     // chain form (chain != 0): F consecutive buckets of a sweep fused in
-    // registers; chain = F | gmask << 8 | form << 16 (bnpp_device.h, ChainForm)
+    // registers; chain = F | gmask << 8 | form << 16 | dep << 20 (ChainForm, ChainDep)
     int32_t chain, chain_pad;
 };
 
@@ -101,7 +104,17 @@ __host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 409
 //              contiguous K^F block per entry of the rest), the output holds
 //              n_j at slab strides; 16 B of the rest's fastest dim per thread
 enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2 };
-__host__ __device__ inline int chain_key(int form, int k, int f) { return 8192 + form * 256 + k * 16 + f; }
+// Which slots G_j depends on besides its own (x_j, n_j): the next slot (j+1,
+// e.g. a forward sweep's vertical factor), the previous one (j-1, backward),
+// or any (every G value of a bucket fetched separately; small tables only).
+enum ChainDep : int32_t { kDepNext = 0, kDepPrev = 1, kDepAny = 2 };
+__host__ __device__ inline int chain_key(int form, int k, int f, int dep) {
+    return 8192 + dep * 2048 + form * 256 + k * 16 + f;
+}
+// rest entries per thread of the backward form (the forward form has 1)
+__host__ __device__ constexpr int chain_bwd_v(int n, int elem_bytes) {
+    return 64 / n < 1 ? 1 : (64 / n > 16 / elem_bytes ? 16 / elem_bytes : 64 / n);
+}
 // chain pool rows: per rest dim (fastest first) 4 + F words
 //   w0 header  w1 magic  w2 input stride  w3 output stride  w4.. G_j stride (j < F)
 // then per slot p: input stride, output stride (2F words); then per bucket j:

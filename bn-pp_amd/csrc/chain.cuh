@@ -50,6 +50,12 @@ struct ChainShape {
     }
 };
 
+__device__ __forceinline__ int64_t readfirstlane64(int64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x & 0xffffffffu));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 template <int F>
 struct ChainState {
     const void *big;
@@ -134,37 +140,44 @@ __device__ __forceinline__ void chain_stage(const BucketDesc &d, TableMeta *meta
 }
 
 // Bucket J of a run on the register table t (MODE 0: no factor tables,
-// 1: G_J shared by the thread's V rest entries, 2: G_J varies along them).
-// Every G value the bucket needs is fetched from LDS before any is used (one
-// wait), then each output entry is  acc = 0; acc += G * m  over x_J = 0..K-1.
-template <typename T, int K, int F, int V, int J, int MODE>
-__device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small, int32_t gb, int32_t gv,
+// 1: G_J, the same for the thread's V rest entries).  Every G value the bucket
+// needs is fetched from LDS before any is used (one wait); then each output
+// entry is  acc = 0; acc += G * m  over x_J = 0..K-1.  DEP (ChainDep) says
+// which other slot G_J may vary with, so only K^3 values are fetched (any:
+// one per (other slots, x, n)).
+template <typename T, int K, int F, int V, int J, int MODE, int DEP>
+__device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small, int32_t gb,
                                            const int32_t (&gs)[F], int32_t gsn) {
     using S = ChainShape<K, F>;
     constexpr int N = S::N;
     constexpr int PJ = S::place(J);
     constexpr int NA = N / K;                       // assignments of the other slots
-    constexpr int NG = MODE == 2 ? V : 1;
-    T g[MODE == 0 ? 1 : NA][K][K][NG];
+    constexpr int Q = DEP == kDepNext ? J + 1 : DEP == kDepPrev ? J - 1 : -1;   // neighbour slot
+    constexpr bool HASQ = Q >= 0 && Q < F;
+    constexpr int NG = MODE == 0 ? 1 : DEP == kDepAny ? NA : (HASQ ? K : 1);
+    T g[NG][K][K];
     if constexpr (MODE != 0) {
-        static_for<NA>([&](auto ic) {
-            constexpr int ai = decltype(ic)::value;
-            constexpr int a = (ai / PJ) * PJ * K + ai % PJ;          // slot J digit 0
+        static_for<NG>([&](auto ic) {
+            constexpr int gi = decltype(ic)::value;
             int32_t go = gb;
+            if constexpr (DEP == kDepAny) {
+                constexpr int a = (gi / PJ) * PJ * K + gi % PJ;          // slot J digit 0
 #pragma unroll
-            for (int p = 0; p < F; ++p)
-                if (p != J) go += S::digit(a, p) * gs[p];
+                for (int p = 0; p < F; ++p)
+                    if (p != J) go += S::digit(a, p) * gs[p];
+            } else if constexpr (HASQ) {
+                go += gi * gs[Q];
+            }
 #pragma unroll
             for (int n = 0; n < K; ++n)
 #pragma unroll
-                for (int x = 0; x < K; ++x)
-#pragma unroll
-                    for (int v = 0; v < NG; ++v) g[ai][n][x][v] = small[go + x * gs[J] + n * gsn + v * gv];
+                for (int x = 0; x < K; ++x) g[gi][n][x] = small[go + x * gs[J] + n * gsn];
         });
     }
     static_for<NA>([&](auto ic) {
         constexpr int ai = decltype(ic)::value;
         constexpr int a = (ai / PJ) * PJ * K + ai % PJ;
+        constexpr int gi = MODE == 0 ? 0 : DEP == kDepAny ? ai : (HASQ ? S::digit(a, HASQ ? Q : 0) : 0);
         T nw[K][V];
 #pragma unroll
         for (int n = 0; n < K; ++n) {
@@ -176,8 +189,7 @@ __device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small
                 for (int v = 0; v < V; ++v) {
                     const T m = t[a + x * PJ][v];
                     T p = m;
-                    if constexpr (MODE == 1) p = g[ai][n][x][0] * m;
-                    if constexpr (MODE == 2) p = g[ai][n][x][v] * m;
+                    if constexpr (MODE == 1) p = g[gi][n][x] * m;
                     nw[n][v] = nw[n][v] + p;
                 }
             }
@@ -189,18 +201,32 @@ __device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small
     });
 }
 
+// per-wave LDS image of the forward form: 64 rows of K^F entries (+16 B pad)
+template <typename T, int K, int F>
+constexpr int chain_img_wave() { return 64 * (ipow(K, F) * (int)sizeof(T) + kLdsRowPad); }
+
+// waves per SIMD the register allocation must leave room for (0: compiler's
+// choice).  Measured on the 32x32 sweep: the forward 32-entry run at 3 waves
+// 7.26 -> 6.57 ms per 2^32 message (4 waves spills); the backward runs are
+// best left alone.
 template <typename T, int K, int F, int FORM>
-__global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
+constexpr int chain_min_waves() {
+    return FORM == kChainFwd && sizeof(T) == 4 && ipow(K, F) == 32 ? 3 : 1;
+}
+
+template <typename T, int K, int F, int FORM, int DEP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chain_min_waves<T, K, F, FORM>())))
+void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                              const int64_t *__restrict__ pool,
                                                              TableMeta *__restrict__ meta, int64_t total_vblocks) {
     using S = ChainShape<K, F>;
     constexpr int N = S::N;
-    constexpr int V = FORM == kChainFwd ? 1 : 16 / (int)sizeof(T);   // entries of the rest per thread
-    static_assert(FORM != kChainFwd || N * (int)sizeof(T) <= 64, "forward rows go through the 64-B LDS image");
+    constexpr int V = FORM == kChainFwd ? 1 : chain_bwd_v(N, (int)sizeof(T));   // rest entries per thread
+    static_assert(FORM != kChainFwd || N * (int)sizeof(T) <= 128, "forward rows go through the wave's LDS image");
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
     unsigned char *stage = dyn + kRedBytes;
-    constexpr int kImg = FORM == kChainFwd ? (kBlock / 64) * kLdsWaveBytes : 0;
+    constexpr int kImg = FORM == kChainFwd ? (kBlock / 64) * chain_img_wave<T, K, F>() : 0;
     T *small = reinterpret_cast<T *>(dyn + kRedBytes + kImg);
 
     ChainState<F> c;
@@ -254,12 +280,16 @@ __global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *_
             const T *big = static_cast<const T *>(c.big);
             if constexpr (FORM == kChainFwd) {
                 // one slab per slot assignment: scalar loads, coalesced over the wave
+                // slab base uniform (SGPRs), lane offset 32-bit (planner: kChainLo32)
+                const int64_t w0 = readfirstlane64(in_off);
+                const uint32_t lob = (uint32_t)((in_off - w0) * (int64_t)sizeof(T));
+                const char *wb = reinterpret_cast<const char *>(big + w0);
 #pragma unroll
                 for (int a = 0; a < N; ++a) {
-                    int64_t o = in_off;
+                    int64_t o = 0;
 #pragma unroll
                     for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.is[p];
-                    t[a][0] = gload(big + o);
+                    t[a][0] = gload(reinterpret_cast<const T *>(wb + o * (int64_t)sizeof(T) + lob));
                 }
             } else {
                 // K^F contiguous entries (slot 0 fastest) per rest entry
@@ -274,10 +304,10 @@ __global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *_
             // the F buckets of the run, in order
             static_for<F>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                if (!((c.gmask >> j) & 1))
-                    chain_step<T, K, F, V, j, 0>(t, small, gb[j], gv[j], c.gs[j], c.gsn[j]);
+                if (!((c.gmask >> j) & 1))                     // uniform
+                    chain_step<T, K, F, V, j, 0, DEP>(t, small, gb[j], c.gs[j], c.gsn[j]);
                 else                       // V > 1: G_j constant along the V entries (planner-checked)
-                    chain_step<T, K, F, V, j, 1>(t, small, gb[j], gv[j], c.gs[j], c.gsn[j]);
+                    chain_step<T, K, F, V, j, 1, DEP>(t, small, gb[j], c.gs[j], c.gsn[j]);
             });
             if (c.flags & kScale) {
 #pragma unroll
@@ -291,12 +321,15 @@ __global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *_
                 for (int v = 0; v < V; ++v) lmax = t[a][v] > lmax ? t[a][v] : lmax;
             if constexpr (FORM == kChainBwd) {
                 T *out = static_cast<T *>(c.out);
+                const int64_t w0 = readfirstlane64(out_off);       // planner: kChainLo32
+                const uint32_t lob = (uint32_t)((out_off - w0) * (int64_t)sizeof(T));
+                char *wb = reinterpret_cast<char *>(out + w0);
 #pragma unroll
                 for (int a = 0; a < N; ++a) {
-                    int64_t o = out_off;
+                    int64_t o = 0;
 #pragma unroll
                     for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.os[p];
-                    store_n<T, V, kNtStore, true>(out + o, t[a]);
+                    store_n<T, V, kNtStore, true>(reinterpret_cast<T *>(wb + o * (int64_t)sizeof(T) + lob), t[a]);
                 }
             }
         }
@@ -306,27 +339,38 @@ __global__ __launch_bounds__(kBlock) void chain_level_kernel(const BucketDesc *_
 #pragma unroll
             for (int a = 0; a < N; ++a) row[a] = t[a][0];
             store_tiles<T, N>(static_cast<T *>(c.out), tid0 + (threadIdx.x & ~63), c.n_tiles, row,
-                              stage + (threadIdx.x >> 6) * kLdsWaveBytes);
+                              stage + (threadIdx.x >> 6) * chain_img_wave<T, K, F>());
         }
     }
     if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
 }
 
-template <typename T, int K, int F, int FORM>
+template <typename T, int K, int F, int FORM, int DEP>
 static hipError_t go_chain_level(const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream) {
     const int64_t grid = a.vblocks < max_grid ? a.vblocks : max_grid;
-    const size_t img = FORM == kChainFwd ? (size_t)(kBlock / 64) * kLdsWaveBytes : 0;
+    const size_t img = FORM == kChainFwd ? (size_t)(kBlock / 64) * chain_img_wave<T, K, F>() : 0;
     const size_t shm = kRedBytes + img + (size_t)small_elems * sizeof(T);
-    hipLaunchKernelGGL((chain_level_kernel<T, K, F, FORM>), dim3((unsigned)grid), dim3(kBlock), shm, stream, a.descs,
-                       a.n_desc, a.pool, a.meta, a.vblocks);
+    hipLaunchKernelGGL((chain_level_kernel<T, K, F, FORM, DEP>), dim3((unsigned)grid), dim3(kBlock), shm, stream,
+                       a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
     return hipGetLastError();
 }
 
-#define BNPP_CASE_CHAIN(T, K, F, FORM) \
-    case 8192 + FORM * 256 + K * 16 + F: return go_chain_level<T, K, F, FORM>(a, small_elems, max_grid, stream);
-// instantiated shapes (planner: kChainMaxN per dtype)
-#define BNPP_CHAIN_F32(X, T) X(T, 2, 2, 1) X(T, 2, 3, 1) X(T, 2, 4, 1) X(T, 4, 2, 1) \
-    X(T, 2, 2, 2) X(T, 2, 3, 2) X(T, 2, 4, 2) X(T, 4, 2, 2)
-#define BNPP_CHAIN_F64(X, T) X(T, 2, 2, 1) X(T, 2, 3, 1) X(T, 2, 2, 2) X(T, 2, 3, 2)
+#define BNPP_CASE_CHAIN(T, K, F, FORM, DEP) \
+    case 8192 + DEP * 2048 + FORM * 256 + K * 16 + F: return go_chain_level<T, K, F, FORM, DEP>(a, small_elems, max_grid, stream);
+#define BNPP_CASE_CHAIN_OK(T, K, F, FORM, DEP) case 8192 + DEP * 2048 + FORM * 256 + K * 16 + F: return true;
+// instantiated shapes: forward rows <= 128 B, backward tables <= 64 entries
+// (V = 1 there); dep "any" only for tables <= 16 entries
+#define BNPP_CHAIN_ND(X, T, K, F, FORM) X(T, K, F, FORM, 0) X(T, K, F, FORM, 1)
+#define BNPP_CHAIN_F32(X, T) \
+    BNPP_CHAIN_ND(X, T, 2, 2, 1) BNPP_CHAIN_ND(X, T, 2, 3, 1) BNPP_CHAIN_ND(X, T, 2, 4, 1) BNPP_CHAIN_ND(X, T, 2, 5, 1) \
+    BNPP_CHAIN_ND(X, T, 4, 2, 1) X(T, 2, 2, 1, 2) X(T, 2, 3, 1, 2) X(T, 2, 4, 1, 2) X(T, 4, 2, 1, 2) \
+    BNPP_CHAIN_ND(X, T, 2, 2, 2) BNPP_CHAIN_ND(X, T, 2, 3, 2) BNPP_CHAIN_ND(X, T, 2, 4, 2) BNPP_CHAIN_ND(X, T, 2, 5, 2) \
+    BNPP_CHAIN_ND(X, T, 2, 6, 2) BNPP_CHAIN_ND(X, T, 4, 2, 2) BNPP_CHAIN_ND(X, T, 4, 3, 2) \
+    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) X(T, 2, 4, 2, 2) X(T, 4, 2, 2, 2)
+#define BNPP_CHAIN_F64(X, T) \
+    BNPP_CHAIN_ND(X, T, 2, 2, 1) BNPP_CHAIN_ND(X, T, 2, 3, 1) BNPP_CHAIN_ND(X, T, 2, 4, 1) \
+    X(T, 2, 2, 1, 2) X(T, 2, 3, 1, 2) \
+    BNPP_CHAIN_ND(X, T, 2, 2, 2) BNPP_CHAIN_ND(X, T, 2, 3, 2) BNPP_CHAIN_ND(X, T, 2, 4, 2) BNPP_CHAIN_ND(X, T, 2, 5, 2) \
+    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2)
 
 }  // namespace bnpp

@@ -7,4 +7,8 @@ hipError_t dispatch_chain_level_f64(int key, const LevelArgs &a, int small_elems
     switch (key) { BNPP_CHAIN_F64(BNPP_CASE_CHAIN, double) default: break; }
     return hipErrorInvalidValue;
 }
+bool chain_supported_f64(int key) {
+    switch (key) { BNPP_CHAIN_F64(BNPP_CASE_CHAIN_OK, double) default: break; }
+    return false;
+}
 }  // namespace bnpp

@@ -132,7 +132,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         if (cards[b.chain_x[j]] != K || cards[b.chain_n[j]] != K) return fail("chain: mixed cardinalities");
         N *= K;
     }
-    if (N > chain_max_entries(eb) || (K != 2 && K != 4)) return fail("chain: register table too large");
+    if (N > 64 || (K != 2 && K != 4)) return fail("chain: register table too large");
     std::vector<int> gidx(F, -1);                     // input index of G_j (-1: absent)
     int ni = 1;
     for (int j = 0; j < F; ++j)
@@ -186,7 +186,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     // kernel form
     int form = 0, V = 1;
     {
-        bool fwd = N * eb <= 64;
+        bool fwd = N * eb <= 128;
         for (int p = 0; fwd && p < F; ++p) {
             int64_t pl = 1;
             for (int q = p + 1; q < F; ++q) pl *= K;
@@ -195,17 +195,35 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         if (fwd && !md.empty()) fwd = md[0].out == N;
         bool bwd = true;
         const int W = eb == 4 ? (N % 4 == 0 ? 4 : N % 2 == 0 ? 2 : 1) : (N % 2 == 0 ? 2 : 1);   // load_n width
-        const int bv = 16 / eb;
+        const int bv = chain_bwd_v(N, eb);
         int64_t pk = 1;
         for (int p = 0; bwd && p < F; ++p, pk *= K) bwd = is[p] == pk;
         bwd = bwd && !md.empty() && md[0].out == 1 && md[0].card % (uint64_t)bv == 0 && big.base % W == 0;
+        if (bv == 1) bwd = bwd && !md.empty() && md[0].out == 1;
         for (const RDim &r : md) bwd = bwd && r.in % W == 0 && (r.out % bv == 0 || &r == &md[0]);
         for (int p = 0; bwd && p < F; ++p) bwd = os[p] % bv == 0;
-        for (int j = 0; bwd && j < F; ++j) bwd = md[0].g[j] == 0;      // G constant along a thread's V entries
+        for (int j = 0; bwd && bv > 1 && j < F; ++j) bwd = md[0].g[j] == 0;   // G constant along a thread's V entries
         if (fwd) form = kChainFwd;
         else if (bwd) { form = kChainBwd; V = bv; }
         else return fail("chain: layout fits no kernel form");
     }
+    // which other slot each G_j varies with (ChainDep)
+    int dep = kDepAny;
+    {
+        bool next = true, prev = true;
+        for (int j = 0; j < F; ++j) {
+            if (gidx[j] < 0) continue;
+            for (int p = 0; p < F; ++p) {
+                if (p == j) continue;
+                const int var = p < j ? b.chain_n[p] : b.chain_x[p];
+                if (stride_of(b.in[gidx[j]], var) == 0) continue;
+                if (p != j + 1) next = false;
+                if (p != j - 1) prev = false;
+            }
+        }
+        dep = next ? kDepNext : prev ? kDepPrev : kDepAny;
+    }
+    if (!chain_supported(eb, chain_key(form, K, F, dep))) return fail("chain: shape not instantiated");
     d = BucketDesc{};
     d.out_size = rest * N;
     d.n_tiles = rest / V;
@@ -217,7 +235,20 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     d.out_table = b.out_table;
     d.flags = kScale | kTrackMax;
     d.big = -1;
-    d.chain = F | (b.chain_gmask << 8) | (form << 16);
+    d.chain = F | (b.chain_gmask << 8) | (form << 16) | (dep << 20);
+    {
+        // the streamed side linear in the thread index: a wave spans 64 * V
+        // consecutive rest entries -> uniform base + 32-bit lane byte offset
+        bool lin = !md.empty();
+        const bool fwdf = form == kChainFwd;
+        int64_t s0 = md.empty() ? 0 : (fwdf ? md[0].in : md[0].out);
+        for (size_t q = 0; lin && q + 1 < md.size(); ++q) {
+            const int64_t a = fwdf ? md[q].in : md[q].out, nb = fwdf ? md[q + 1].in : md[q + 1].out;
+            lin = nb == a * (int64_t)md[q].card;
+        }
+        if (lin && s0 > 0 && 64 * (int64_t)V * s0 * eb < ((int64_t)1 << 31)) d.flags |= kChainLo32;
+        else return fail("chain: streamed side not linear in the thread index");
+    }
     int32_t lo = 0;
     for (int i = 0; i < kMaxIn; ++i) {
         d.in_table[i] = i < ni ? b.in[i].table : 0;
@@ -516,7 +547,10 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
 }
 
 // ---------------------------------------------------------------- VE plan
-constexpr int kChainRunMax = 4;                   // longest fused run tried (fp32, K = 2)
+constexpr int kChainRunMax = 6;                   // longest fused run tried (fp32, K = 2, backward)
+// first run length to try for `rem` remaining buckets: never leave a single
+// bucket behind when a split into runs >= 2 exists (5 -> 3 + 2, not 4 + 1)
+inline int chain_first_try(int rem) { return rem == kChainRunMax + 1 ? kChainRunMax - 1 : std::min(kChainRunMax, rem); }
 
 namespace {
 // Emits buckets and message tables into a VEPlan (shared by plan_ve and
@@ -623,15 +657,25 @@ struct PlanBuilder {
         for (const ChainStep &st : steps) {
             std::vector<int> u = vars;
             for (const View &v : st.smalls) {
-                if (table_size(v.vars, cards) > kStreamSmallMax) return -1;
+                if (table_size(v.vars, cards) > kStreamSmallMax) {
+                    if (std::getenv("BNPP_DEBUG_CHAIN")) std::fprintf(stderr, "[chain] F=%d: large factor table\n", F);
+                    return -1;
+                }
                 for (int w : v.vars)
                     if (!contains(u, w)) u.push_back(w);
             }
-            if (!contains(vars, st.x) || !contains(big.vars, st.x) || contains(ns, st.x)) return -1;
+            const bool dbg = std::getenv("BNPP_DEBUG_CHAIN") != nullptr;
+            if (!contains(vars, st.x) || !contains(big.vars, st.x) || contains(ns, st.x)) {
+                if (dbg) std::fprintf(stderr, "[chain] F=%d: summed var %d not an input slot\n", F, st.x);
+                return -1;
+            }
             std::vector<int> nw;
             for (int w : u)
                 if (!contains(vars, w)) nw.push_back(w);
-            if (nw.size() != 1 || nw[0] == st.x) return -1;
+            if (nw.size() != 1 || nw[0] == st.x) {
+                if (dbg) std::fprintf(stderr, "[chain] F=%d: bucket brings %zu new variables\n", F, nw.size());
+                return -1;
+            }
             xs.push_back(st.x);
             ns.push_back(nw[0]);
             vars = remove_var(u, st.x);
@@ -657,7 +701,11 @@ struct PlanBuilder {
         {
             BucketDesc d;
             std::vector<int64_t> pool;
-            if (!build_desc(b, cards, chain_eb == 8 ? 2 : 4, d, pool, nullptr)) return -1;
+            std::string why;
+            if (!build_desc(b, cards, chain_eb == 8 ? 2 : 4, d, pool, &why)) {
+                if (std::getenv("BNPP_DEBUG_CHAIN")) std::fprintf(stderr, "[chain] F=%d rejected: %s\n", F, why.c_str());
+                return -1;
+            }
         }
         double moved = (double)table_size(big.vars, cards);
         for (size_t i = 1; i < b.in.size(); ++i) {
@@ -808,7 +856,7 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
         if (B.chain_eb && is_msg(buckets[i].back())) {
             int n_msg = 0;
             for (const View &v : buckets[i]) n_msg += is_msg(v);
-            for (int F = std::min(kChainRunMax, nord - i); F >= 2 && n_msg == 1 && !fused; --F) {
+            for (int F = chain_first_try(nord - i); F >= 2 && n_msg == 1 && !fused; --F) {
                 const View big = buckets[i].back();
                 std::vector<PlanBuilder::ChainStep> steps;
                 std::vector<int> vars = big.vars;
@@ -1113,7 +1161,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             while (jj >= j) {
                 // longest fusable run of backward buckets jj, jj-1, ... (chain.cuh)
                 int fused = 0;
-                for (int F = std::min(kChainRunMax, jj - j + 1); F >= 2 && have_pi && !fused; --F) {
+                for (int F = chain_first_try(jj - j + 1); F >= 2 && have_pi && !fused; --F) {
                     std::vector<PlanBuilder::ChainStep> steps;
                     std::vector<int> vars = pi_cur.vars;
                     for (int i = 0; i < F; ++i) {
@@ -1173,12 +1221,18 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         };
         // lam at position `to` from lam at `from` (-1: from the path's start), streamed
         auto advance = [&](const View *start, int from, int to) {
-            View cur = forward(path[from + 1], start);
-            int k = from + 2;
+            View cur;
+            int k = from + 1;
+            if (start) {
+                cur = *start;
+            } else {                                   // the path's first bucket: no incoming message
+                cur = forward(path[k], nullptr);
+                ++k;
+            }
             while (k <= to) {
                 // longest fusable run of forward buckets k, k+1, ... (chain.cuh)
                 int fused = 0;
-                for (int F = std::min(kChainRunMax, to - k + 1); F >= 2 && !fused; --F) {
+                for (int F = chain_first_try(to - k + 1); F >= 2 && !fused; --F) {
                     std::vector<PlanBuilder::ChainStep> steps;
                     for (int i = 0; i < F; ++i) steps.push_back({src_in[path[k + i]], order[path[k + i]]});
                     const int t = B.emit_chain(cur, steps);
@@ -1190,6 +1244,9 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 if (fused) {
                     k += fused;
                 } else {
+                    if (std::getenv("BNPP_DEBUG_CHAIN"))
+                        std::fprintf(stderr, "[chain] single forward bucket at %d (run %d..%d) vars %zu\n", k, from, to,
+                                     cur.vars.size());
                     cur = forward(path[k], &cur);
                     ++k;
                 }
@@ -1430,7 +1487,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         b.out_table = remap(it.plan, b.out_table);
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
-        it.key = it.d.chain ? chain_key(it.d.chain >> 16, it.d.k, it.d.chain & 0xff)
+        it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf)
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2) : variant_key(it.d.n_in, it.d.v1, it.d.v2);
     });
     for (const Item &it : items)

@@ -54,9 +54,13 @@ struct BucketSpec {
 bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec, BucketDesc &d,
                 std::vector<int64_t> &pool, std::string *msg);
 
-// Fused chain runs: largest K^F register table per element size (kernels
-// instantiated in chain.cuh: fp32 K^F <= 16, fp64 <= 8).
-inline int chain_max_entries(int elem_bytes) { return elem_bytes == 4 ? 16 : 8; }
+// Fused chain runs: is the chain kernel with this key (bnpp_device.h,
+// chain_key) instantiated for this element size (k_chain_f32/f64.hip)?
+bool chain_supported_f32(int key);
+bool chain_supported_f64(int key);
+inline bool chain_supported(int elem_bytes, int key) {
+    return elem_bytes == 4 ? chain_supported_f32(key) : chain_supported_f64(key);
+}
 
 struct MsgTable {
     std::vector<int> vars;
