@@ -7,6 +7,7 @@ to rounding, not bit-exact.  Tolerances: fp64 1e-12 absolute against the
 oracle's marginals and the golden vectors; fp32 1e-5 absolute (north star:
 PR/MAR within 1e-6 relative on Z-scale quantities; marginals are in [0, 1]).
 """
+import math
 import os
 
 import pytest
@@ -197,3 +198,48 @@ def test_tree_chain_fused_runs_identical_to_unfused(ctx, dtype):
     tol = 1e-12 if dtype == bnpp.F64 else 1e-5
     for t in range(m.n_vars):
         assert _close(fused[t], want[t], tol), (t, fused[t], want[t])
+
+
+@pytest.mark.parametrize("dtype", [bnpp.F64, bnpp.F32])
+def test_tree_chain_fused_potts4(ctx, dtype):
+    """4-state Potts column sweep: chain runs over K = 4 slots (16-entry register
+    tables), identical to one bucket per launch and to the per-target engine."""
+    m = bnpp.Model.from_dict(synth.potts_grid(5, 7, k=4, seed=3))
+    col = [r * 7 + c for c in range(7) for r in range(5)]
+    ev = {9: 2}
+    os.environ["BNPP_TREE_SLOTS"] = "2"
+    try:
+        fused, _ = bnpp.marginals_tree(ctx, m, ev, "mf", dtype, order=col)
+        os.environ["BNPP_NO_CHAIN"] = "1"
+        plain, _ = bnpp.marginals_tree(ctx, m, ev, "mf", dtype, order=col)
+    finally:
+        del os.environ["BNPP_TREE_SLOTS"]
+        os.environ.pop("BNPP_NO_CHAIN", None)
+    assert fused == plain
+    want, _ = bnpp.marginals(ctx, m, ev, "mf", bnpp.F64)
+    tol = 1e-12 if dtype == bnpp.F64 else 1e-5
+    for t in range(m.n_vars):
+        assert _close(fused[t], want[t], tol), (t, fused[t], want[t])
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 14), (4, 5, 8)])
+def test_partition_fused_sweep_matches_oracle(ctx, shape):
+    """plan_ve with fused sweep runs (column order): log10 Z bit-identical to
+    one bucket per launch in fp64, and equal to the oracle's Z to 1e-12."""
+    import refcpu
+    k, r, c = shape
+    d = synth.ising_grid(r, c, seed=4) if k == 2 else synth.potts_grid(r, c, k=k, seed=4)
+    m = bnpp.Model.from_dict(d)
+    col = [i * c + j for j in range(c) for i in range(r)]
+    lz, z, _ = bnpp.partition(ctx, m, {}, "mf", bnpp.F64, order=col)
+    os.environ["BNPP_NO_CHAIN"] = "1"
+    try:
+        lz_plain, _, _ = bnpp.partition(ctx, m, {}, "mf", bnpp.F64, order=col)
+        lz32_plain, _, _ = bnpp.partition(ctx, m, {}, "mf", bnpp.F32, order=col)
+    finally:
+        del os.environ["BNPP_NO_CHAIN"]
+    lz32, _, _ = bnpp.partition(ctx, m, {}, "mf", bnpp.F32, order=col)
+    assert lz == lz_plain and lz32 == lz32_plain
+    rz, _ = refcpu.Model.from_dict(d).partition({}, "mf")      # oracle: min-fill order, fp64
+    assert abs(lz - math.log10(rz)) < 1e-12 * abs(lz)
+    assert abs(lz32 - lz) < 1e-6 * abs(lz)
