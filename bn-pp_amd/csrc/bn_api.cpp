@@ -227,6 +227,20 @@ Factor Factor::product(const Factor &f) const {
     return Factor(nd, std::move(vals), p);
 }
 
+Factor Factor::divide(const Factor &f) const {
+    Domain *nd = new Domain(*_domain, *f._domain);                 // same scope rule as product
+    std::vector<int> cards = cards_of({_domain, f._domain});
+    auto a = upload(_values), b = upload(f._values);
+    DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
+    std::vector<int> av = ids(*_domain), bv = ids(*f._domain), ov = ids(*nd);
+    check(bnpp_divide(ctx(), nullptr, BNPP_F64, cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
+                      bv.data(), out.p, (int)ov.size(), ov.data()),
+          "divide");
+    std::vector<double> vals = download(out, nd->size());
+    double p = seq_sum(vals);
+    return Factor(nd, std::move(vals), p);
+}
+
 Factor Factor::sum_out(const Variable *variable) const {
     if (!_domain->in_scope(variable)) return Factor(*this);       // factor.cpp:185-188
     Domain *nd = new Domain(*_domain, variable);
@@ -437,6 +451,29 @@ Factor BN::variable_elimination(std::vector<const Variable *> &variables, std::v
             if ((int)pv->id() == out_vars[i]) scope.push_back(pv);
     double p = seq_sum(vals);
     return Factor(new Domain(scope), std::move(vals), p);
+}
+
+Factor BN::query_ve(const std::unordered_set<const Variable *> &target,
+                    const std::unordered_set<const Variable *> &evidence,
+                    std::unordered_map<std::string, bool> &options, double &uptime) const {
+    // model.cpp:205-248: VE over every variable neither queried nor observed,
+    // then P(target | evidence) = f / sum_target f.  (options["bayes-ball"]
+    // only prunes non-requisite nodes there; the result is the same table.)
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<const Variable *> variables;
+    std::vector<const Factor *> factors;
+    for (auto pv : _variables) {
+        if (!target.count(pv) && !evidence.count(pv)) variables.push_back(pv);
+        factors.push_back(_factors[pv->id()]);
+    }
+    Factor f = variable_elimination(variables, factors, options);
+    if (!evidence.empty()) {
+        Factor g = f;
+        for (auto pv : target) g = g.sum_out(pv);
+        f = f.divide(g);
+    }
+    uptime = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return f;
 }
 
 MN::MN(std::string name, std::vector<Variable *> &variables, std::vector<Factor *> &factors)

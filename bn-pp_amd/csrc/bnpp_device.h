@@ -38,6 +38,7 @@ enum BucketFlags : int32_t {
     kTrackMax = 2,     // raise meta[out].maxbits
     kOutStrided = 4,   // dims permuted: output offset from per-dim output strides
                        // (n_dims words after the dims rows in the pool)
+    kDivide = 16,      // Factor::divide (factor.cpp:149-180): p = in_0 / in_1 instead of the product
     kChainLo32 = 8,    // chain form: the streamed side (forward input / backward output)
                        // is linear in the thread index, so one wave's accesses are a
                        // uniform base + a 32-bit lane offset (saddr addressing)

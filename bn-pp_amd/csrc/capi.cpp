@@ -578,6 +578,35 @@ int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const
     return bnpp_bucket_eliminate(ctx, stream, dtype, cards, 2, tabs, nd, vs, -1, out, out_ndims, out_vars);
 }
 
+int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *a, int a_ndims,
+                const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
+                const int *out_vars) {
+    BNPP_GUARD_BEGIN
+    if (!ctx || !cards || !a || !b || !out || (a_ndims > 0 && !a_vars) || (b_ndims > 0 && !b_vars) ||
+        (out_ndims > 0 && !out_vars))
+        return set_err(BNPP_ERR_INVALID, "null argument");
+    int max_var = -1;
+    for (int j = 0; j < a_ndims; ++j) max_var = std::max(max_var, a_vars[j]);
+    for (int j = 0; j < b_ndims; ++j) max_var = std::max(max_var, b_vars[j]);
+    for (int j = 0; j < out_ndims; ++j) max_var = std::max(max_var, out_vars[j]);
+    std::vector<int> cv(cards, cards + max_var + 1);
+    if (!valid_scope(a_ndims, a_vars, cv.data(), 0) || !valid_scope(b_ndims, b_vars, cv.data(), 0))
+        return set_err(BNPP_ERR_INVALID, "bad input scope");
+    if (!valid_scope(out_ndims, out_vars, cv.data(), 0)) return set_err(BNPP_ERR_INVALID, "bad output scope");
+    BucketSpec bs;
+    bs.in.push_back(natural_view(0, std::vector<int>(a_vars, a_vars + a_ndims), cv));
+    bs.in.push_back(natural_view(1, std::vector<int>(b_vars, b_vars + b_ndims), cv));
+    std::vector<int> u = chain_scope(bs.in), ov(out_vars, out_vars + out_ndims), us = u, os = ov;
+    std::sort(us.begin(), us.end());
+    std::sort(os.begin(), os.end());
+    if (us != os) return set_err(BNPP_ERR_INVALID, "output scope must be the union of the inputs");
+    bs.out_vars = ov;
+    bs.out_table = 2;
+    bs.divide = true;
+    return run_single(ctx, stream, dtype, cv, bs, {a, b}, out);
+    BNPP_GUARD_END
+}
+
 int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
                  const int *vars, int var, void *out, int out_ndims, const int *out_vars) {
     const void *tabs[1] = {in};

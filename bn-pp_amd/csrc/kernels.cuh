@@ -272,8 +272,13 @@ __device__ __forceinline__ T compute_tile(const LoadedBucket &b, int64_t tid, T 
             if (i >= b.n_in) continue;                     // uniform
             T x[TS];
             load_tile<T, V1, V2>(static_cast<const T *>(b.ptr[i]) + pos[i] + (int64_t)v * b.es[i], b.s0[i], b.s1[i], x);
+            if (i == 1 && (b.flags & kDivide)) {          // (*this)[pos1] / f[pos2], factor.cpp:166
 #pragma unroll
-            for (int j = 0; j < TS; ++j) p[j] = p[j] * x[j];
+                for (int j = 0; j < TS; ++j) p[j] = p[j] / x[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < TS; ++j) p[j] = p[j] * x[j];
+            }
         }
 #pragma unroll
         for (int j = 0; j < TS; ++j) acc[j] = acc[j] + p[j];
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(kBlock) void bucket_single_kernel(const SingleArgs 
     const BucketDesc &d = a.d;
     LoadedBucket b;
     load_common(b, d, a.pool);
-    b.flags = 0;
+    b.flags = d.flags & kDivide;
     b.neg_e = 0;
     b.out = a.meta[d.n_in].ptr;
     for (int i = 0; i < kMaxIn; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : nullptr;

@@ -435,7 +435,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         }
         const int eb = max_vec == 2 ? 8 : 4;
         const char *off = std::getenv("BNPP_NO_STREAM");
-        if (n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 && !(off && *off == '1')) {
+        if (!b.divide && n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 && !(off && *off == '1')) {
             int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
             int64_t s1 = merged.size() < 2 ? 0 : merged[1].s[big];
             // optional narrow tile: when the big input is constant along the
@@ -531,6 +531,13 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
             }
             d.small_elems = o;
         }
+    }
+    if (b.divide) {
+        if (n != 2 || b.elim_var >= 0) {
+            if (msg) *msg = "divide takes two inputs and sums nothing";
+            return false;
+        }
+        d.flags |= kDivide;
     }
     d.dim_off = (int64_t)pool.size();
     for (const Dim &dm : merged) {

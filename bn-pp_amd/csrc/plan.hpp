@@ -47,6 +47,7 @@ struct BucketSpec {
     // in[1..] are the G tables of the buckets whose bit is set in chain_gmask
     std::vector<int> chain_x, chain_n;
     int chain_gmask = 0;
+    bool divide = false;            // Factor::divide: in[0] / in[1] (generic kernel, no sum)
 };
 
 // Compile one bucket into a descriptor + dims-pool rows.  max_vec: 4 (fp32) / 2 (fp64).

@@ -53,6 +53,7 @@ _SIGS = {
     "bnpp_out_scope": (_I, [_I, _IP, C.POINTER(_IP), _I, _I, _IP, _IP]),
     "bnpp_bucket_eliminate": (_I, [_P, _P, _I, _IP, _I, C.POINTER(_P), _IP, C.POINTER(_IP), _I, _P, _I, _IP]),
     "bnpp_product": (_I, [_P, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP]),
+    "bnpp_divide": (_I, [_P, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP]),
     "bnpp_sum_out": (_I, [_P, _P, _I, _IP, _P, _I, _IP, _I, _P, _I, _IP]),
     "bnpp_condition": (_I, [_P, _P, _I, _IP, _P, _I, _IP, _I, _IP, _IP, _P]),
     "bnpp_model_load_uai": (_I, [C.c_char_p, C.POINTER(_P)]),
@@ -384,6 +385,15 @@ def bucket_eliminate(ctx: Context, dtype: int, cards: Sequence[int], tables: Seq
     _check(_lib.bnpp_bucket_eliminate(ctx.handle, _P(stream) if stream else None, dtype, _ints(cards), len(tables),
                                       tabs, _ints([len(s) for s in scopes]), ptrs, elim, _P(out), len(out_vars),
                                       _ints(out_vars)), "bnpp_bucket_eliminate")
+
+
+def divide(ctx: Context, dtype: int, cards: Sequence[int], a: int, a_scope: Sequence[int], b: int,
+           b_scope: Sequence[int], out: int, out_vars: Sequence[int], stream: Optional[int] = None) -> None:
+    """Factor::divide (factor.cpp:149-180) on caller-owned device buffers:
+    out = a / b over the union scope (out_vars in any order of it)."""
+    _check(_lib.bnpp_divide(ctx.handle, _P(stream) if stream else None, dtype, _ints(cards), _P(a), len(a_scope),
+                            _ints(a_scope), _P(b), len(b_scope), _ints(b_scope), _P(out), len(out_vars),
+                            _ints(out_vars)), "bnpp_divide")
 
 
 def condition(ctx: Context, dtype: int, cards: Sequence[int], table: int, scope: Sequence[int],

@@ -96,6 +96,13 @@ int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const
                  const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
                  const int *out_vars);
 
+/* Factor::divide (factor.cpp:149-180; factor.hh:36): out = a / b over the
+ * union scope (out_vars: any order of it).  The reference asserts on a zero
+ * divisor (factor.cpp:165); here it yields inf / nan in that entry. */
+int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *a, int a_ndims,
+                const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
+                const int *out_vars);
+
 /* Factor::sum_out (factor.cpp:182-212; factor.hh:34) */
 int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
                  const int *vars, int var, void *out, int out_ndims, const int *out_vars);

@@ -85,6 +85,7 @@ public:
 
     Factor sum_out(const Variable *variable) const;                                  // factor.cpp:182-212
     Factor product(const Factor &f) const;                                           // factor.cpp:117-147
+    Factor divide(const Factor &f) const;                                            // factor.cpp:149-180
     Factor conditioning(const std::unordered_map<unsigned, unsigned> &evidence) const;  // factor.cpp:214-242
     Factor normalize() const;                                                        // factor.cpp:244-255
     friend std::ostream &operator<<(std::ostream &os, const Factor &f);
@@ -132,6 +133,10 @@ public:
     // model.cpp:348-446: bucket elimination, one fused GPU kernel per bucket
     Factor variable_elimination(std::vector<const Variable *> &variables, std::vector<const Factor *> &factors,
                                 std::unordered_map<std::string, bool> &options) const;
+    // model.cpp:205-248: P(target | evidence) as a table over target + evidence
+    Factor query_ve(const std::unordered_set<const Variable *> &target,
+                    const std::unordered_set<const Variable *> &evidence,
+                    std::unordered_map<std::string, bool> &options, double &uptime) const;
     const std::unordered_set<const Variable *> parents(const Variable *v) const { return _parents.find(v)->second; }
     const std::unordered_set<const Variable *> children(const Variable *v) const { return _children.find(v)->second; }
 

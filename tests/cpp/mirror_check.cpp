@@ -7,6 +7,7 @@
 #include <iostream>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "bnpp/bn.hpp"
@@ -64,6 +65,42 @@ int main(int argc, char **argv) {
         delete m2[i];
     }
     delete mn;
+
+    // Factor::divide (factor.cpp:149-180) against the explicit loop: scope (a, b, c)
+    Factor q = p.divide(g);
+    CHECK(q.width() == 3 && q.size() == 12);
+    for (unsigned ia = 0; ia < 2; ++ia)
+        for (unsigned ib = 0; ib < 3; ++ib)
+            for (unsigned ic = 0; ic < 2; ++ic)
+                CHECK(q[(ia * 3 + ib) * 2 + ic] == p[(ia * 3 + ib) * 2 + ic] / gv[ib * 2 + ic]);
+
+    // BN::query_ve (model.cpp:205-248) on asia: P(t | e) as a table over (t, e);
+    // each column e = v equals the marginal of t under evidence {e: v}
+    std::string asia = dir + "/asia.uai";
+    BN *bn = nullptr;
+    CHECK(read_uai_model(asia, &bn) == 0);
+    if (bn) {
+        const std::vector<Variable *> &vs = bn->variables();
+        const Variable *t = vs[1], *e = vs[5];
+        std::unordered_set<const Variable *> target{t}, evidence{e};
+        std::unordered_map<std::string, bool> opt{{"min-fill", true}};
+        Factor qv = bn->query_ve(target, evidence, opt, up);
+        CHECK(qv.width() == 2 && qv.size() == t->size() * e->size());
+        const bool t_first = qv.domain()[0] == t;
+        for (unsigned v = 0; v < e->size(); ++v) {
+            std::unordered_map<unsigned, unsigned> evv{{e->id(), v}};
+            std::vector<const Factor *> mv = bn->marginals(evv, opt, up);
+            double colsum = 0;
+            for (unsigned x = 0; x < t->size(); ++x) {
+                double got = t_first ? qv[x * e->size() + v] : qv[v * t->size() + x];
+                colsum += got;
+                CHECK(std::fabs(got - (*mv[t->id()])[x]) < 1e-12);
+            }
+            CHECK(std::fabs(colsum - 1.0) < 1e-12);
+            for (auto m : mv) delete m;
+        }
+        delete bn;
+    }
     if (fails) return 1;
     std::cout << "OK" << std::endl;
     return 0;

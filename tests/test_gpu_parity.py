@@ -98,8 +98,20 @@ def test_kat_single_ops(ctx, golden_kat, dtype):
                            stream=_stream())
             torch.cuda.synchronize()
             vals = out.cpu().tolist()
+        elif op == "divide":              # Factor::divide (factor.cpp:149-180), bnpp_divide
+            a, b = facs[case["a"]], facs[case["b"]]
+            scope = ref["scope"]
+            size = 1
+            for v in scope:
+                size *= cards[v]
+            ta, tb = _dev(a["values"], dtype), _dev(b["values"], dtype)
+            out = torch.full((size,), float("nan"), dtype=TD[dtype], device=DEV)
+            bnpp.divide(ctx, dtype, _cards_list(cards), ta.data_ptr(), a["scope"], tb.data_ptr(), b["scope"],
+                        out.data_ptr(), scope, stream=_stream())
+            torch.cuda.synchronize()
+            vals = out.cpu().tolist()
         else:
-            continue                      # normalize / divide: host bookkeeping, not on the device path
+            continue                      # normalize: host bookkeeping (width <= 1 in MAR)
         assert scope == ref["scope"], case
         if dtype == bnpp.F64:
             assert vals == ref["values"], case
@@ -107,7 +119,7 @@ def test_kat_single_ops(ctx, golden_kat, dtype):
             for x, y in zip(vals, ref["values"]):
                 assert abs(x - y) <= 1e-6 * abs(y) + 1e-30, (case, x, y)
         checked += 1
-    assert checked >= 200
+    assert checked >= 260
 
 
 def _rand_bucket(rng, n_vars=12):
