@@ -495,15 +495,16 @@ template <typename T, int V1, int V2, int BC>
 struct BigTile {
     static constexpr int TS = V1 * V2;
     static constexpr int N = BC == kBigRow ? V1 : BC == kBigCol ? V2 : (BC == kBigOne || BC >= kBigInter2) ? 1 : TS;
+    template <bool NTL>
     static __device__ __forceinline__ void issue(const T *src, int64_t s0, int64_t s1, T (&buf)[N]) {
         if constexpr (BC == kBigOne) {
             buf[0] = gload(src);
         } else if constexpr (BC == kBigRow) {
-            load_n<T, V1, kNtLoad, true>(src, buf);
+            load_n<T, V1, NTL, true>(src, buf);
         } else if constexpr (BC == kBigCol) {
-            load_n<T, V2, kNtLoad, true>(src, buf);
+            load_n<T, V2, NTL, true>(src, buf);
         } else if constexpr (BC == kBigFull) {
-            load_n<T, TS, kNtLoad, true>(src, buf);
+            load_n<T, TS, NTL, true>(src, buf);
         } else {
 #pragma unroll
             for (int j2 = 0; j2 < V2; ++j2)
@@ -530,7 +531,10 @@ struct StreamState {
     int32_t span[kMaxIn];
 };
 
-template <typename T, int V1, int V2, int BC>
+// NTL: nontemporal loads of the big input -- the single-op calls (cold, user
+// tables: measured -2 % on the bench bucket); level kernels keep kNtLoad (a
+// VE chain re-reads the message the previous bucket just wrote)
+template <typename T, int V1, int V2, int BC, bool NTL>
 __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const StreamState &st, const T *small,
                                                  int64_t tid, T (&acc)[V1 * V2], int64_t &out_off) {
     constexpr bool kRows = (BC == kBigInter2 || BC == kBigInter4) && V2 > 1;   // output rows at a stride
@@ -631,7 +635,7 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
         // contiguous values, fetched by one vector load (V2 == 1)
         constexpr int K = BC == kBigInter2 ? 2 : 4;
         T all[V1 * K];
-        load_n<T, V1 * K, kNtLoad, true>(bsrc, all);
+        load_n<T, V1 * K, NTL, true>(bsrc, all);
 #pragma unroll
         for (int v = 0; v < K; ++v) {
             T p[TS];
@@ -656,7 +660,7 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
             T bb[U][BT::N];
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (v0 + u < b.k) BT::issue(bsrc + (int64_t)(v0 + u) * bes, bs0, bs1, bb[u]);
+                if (v0 + u < b.k) BT::template issue<NTL>(bsrc + (int64_t)(v0 + u) * bes, bs0, bs1, bb[u]);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int v = v0 + u;
@@ -808,7 +812,7 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_level_ker
         T acc[V1 * V2];
         int64_t oo = 0;
         if (tid < b.n_tiles) {
-            T m = compute_stream_tile<T, V1, V2, BC>(b, st, small, tid, acc, oo);
+            T m = compute_stream_tile<T, V1, V2, BC, kNtLoad>(b, st, small, tid, acc, oo);
             lmax = m > lmax ? m : lmax;
         }
         stream_store<T, V1, V2, BC>(b, tid0, tid, oo, acc, stage);
@@ -841,7 +845,7 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_single_ke
         const int64_t tid = tid0 + threadIdx.x;
         T acc[V1 * V2];
         int64_t oo = 0;
-        if (tid < b.n_tiles) (void)compute_stream_tile<T, V1, V2, BC>(b, st, small, tid, acc, oo);
+        if (tid < b.n_tiles) (void)compute_stream_tile<T, V1, V2, BC, true>(b, st, small, tid, acc, oo);
         stream_store<T, V1, V2, BC>(b, tid0, tid, oo, acc, stage);
     }
 }
