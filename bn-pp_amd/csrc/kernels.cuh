@@ -841,7 +841,9 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_single_ke
     b.out = a.meta[d.n_in].ptr;
     for (int i = 0; i < kMaxIn; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : nullptr;
     stage_small<T>(b, st, small);
-    for (int64_t tid0 = (int64_t)blockIdx.x * kBlock; tid0 < b.n_tiles; tid0 += (int64_t)gridDim.x * kBlock) {
+    const int64_t gstride = (int64_t)gridDim.x * kBlock;
+    int64_t tid0 = (int64_t)blockIdx.x * kBlock;
+    for (; tid0 < b.n_tiles; tid0 += gstride) {
         const int64_t tid = tid0 + threadIdx.x;
         T acc[V1 * V2];
         int64_t oo = 0;

@@ -1,2 +1,2 @@
 set -o pipefail
-bash tools/ab_libs.sh base mw6 mw8 base mw6 mw8 > gpurun_out/ab4.txt 2>&1
+bash tools/ab_libs.sh base x2 base x2 > gpurun_out/ab5.txt 2>&1
