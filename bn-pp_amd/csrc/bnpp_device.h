@@ -104,7 +104,10 @@ __host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 409
 //   kChainBwd: x_j are the input's fastest variables (slot 0 fastest: one
 //              contiguous K^F block per entry of the rest), the output holds
 //              n_j at slab strides; 16 B of the rest's fastest dim per thread
-enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2 };
+//   kChainSum: every bucket only sums its variable out (no new variable: the
+//              last column of a sweep); slots are the input's slabs, V rest
+//              entries per thread contiguous in input and output
+enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2, kChainSum = 3 };
 // Which slots G_j depends on besides its own (x_j, n_j): the next slot (j+1,
 // e.g. a forward sweep's vertical factor), the previous one (j-1, backward),
 // or any (every G value of a bucket fetched separately; small tables only).

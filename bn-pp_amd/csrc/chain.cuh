@@ -145,17 +145,20 @@ __device__ __forceinline__ void chain_stage(const BucketDesc &d, TableMeta *meta
 // entry is  acc = 0; acc += G * m  over x_J = 0..K-1.  DEP (ChainDep) says
 // which other slot G_J may vary with, so only K^3 values are fetched (any:
 // one per (other slots, x, n)).
-template <typename T, int K, int F, int V, int J, int MODE, int DEP>
+// SUM: the bucket only sums x_J out (no new variable): slots < J were summed
+// before and hold digit 0; only digit 0 of slot J is written.
+template <typename T, int K, int F, int V, int J, int MODE, int DEP, bool SUM = false>
 __device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small, int32_t gb,
                                            const int32_t (&gs)[F], int32_t gsn) {
     using S = ChainShape<K, F>;
     constexpr int N = S::N;
     constexpr int PJ = S::place(J);
     constexpr int NA = N / K;                       // assignments of the other slots
+    constexpr int NK = SUM ? 1 : K;                 // values of the new variable
     constexpr int Q = DEP == kDepNext ? J + 1 : DEP == kDepPrev ? J - 1 : -1;   // neighbour slot
     constexpr bool HASQ = Q >= 0 && Q < F;
     constexpr int NG = MODE == 0 ? 1 : DEP == kDepAny ? NA : (HASQ ? K : 1);
-    T g[NG][K][K];
+    T g[NG][NK][K];
     if constexpr (MODE != 0) {
         static_for<NG>([&](auto ic) {
             constexpr int gi = decltype(ic)::value;
@@ -169,7 +172,7 @@ __device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small
                 go += gi * gs[Q];
             }
 #pragma unroll
-            for (int n = 0; n < K; ++n)
+            for (int n = 0; n < NK; ++n)
 #pragma unroll
                 for (int x = 0; x < K; ++x) g[gi][n][x] = small[go + x * gs[J] + n * gsn];
         });
@@ -177,10 +180,11 @@ __device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small
     static_for<NA>([&](auto ic) {
         constexpr int ai = decltype(ic)::value;
         constexpr int a = (ai / PJ) * PJ * K + ai % PJ;
+        if constexpr (SUM && (a / (PJ * K)) != 0) return;    // a slot summed earlier is not 0: dead entry
         constexpr int gi = MODE == 0 ? 0 : DEP == kDepAny ? ai : (HASQ ? S::digit(a, HASQ ? Q : 0) : 0);
-        T nw[K][V];
+        T nw[NK][V];
 #pragma unroll
-        for (int n = 0; n < K; ++n) {
+        for (int n = 0; n < NK; ++n) {
 #pragma unroll
             for (int v = 0; v < V; ++v) nw[n][v] = T(0);
 #pragma unroll
@@ -195,7 +199,7 @@ __device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small
             }
         }
 #pragma unroll
-        for (int n = 0; n < K; ++n)
+        for (int n = 0; n < NK; ++n)
 #pragma unroll
             for (int v = 0; v < V; ++v) t[a + n * PJ][v] = nw[n][v];
     });
@@ -221,7 +225,8 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                              TableMeta *__restrict__ meta, int64_t total_vblocks) {
     using S = ChainShape<K, F>;
     constexpr int N = S::N;
-    constexpr int V = FORM == kChainFwd ? 1 : chain_bwd_v(N, (int)sizeof(T));   // rest entries per thread
+    constexpr bool SUM = FORM == kChainSum;
+    constexpr int V = FORM == kChainFwd ? 1 : SUM ? 16 / (int)sizeof(T) : chain_bwd_v(N, (int)sizeof(T));
     static_assert(FORM != kChainFwd || N * (int)sizeof(T) <= 128, "forward rows go through the wave's LDS image");
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
@@ -278,7 +283,19 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                 dp += row;
             }
             const T *big = static_cast<const T *>(c.big);
-            if constexpr (FORM == kChainFwd) {
+            if constexpr (SUM) {
+                // one slab per slot assignment, V contiguous rest entries each
+                const int64_t w0 = readfirstlane64(in_off);
+                const uint32_t lob = (uint32_t)((in_off - w0) * (int64_t)sizeof(T));
+                const char *wb = reinterpret_cast<const char *>(big + w0);
+#pragma unroll
+                for (int a = 0; a < N; ++a) {
+                    int64_t o = 0;
+#pragma unroll
+                    for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.is[p];
+                    load_n<T, V, kNtLoad, true>(reinterpret_cast<const T *>(wb + o * (int64_t)sizeof(T) + lob), t[a]);
+                }
+            } else if constexpr (FORM == kChainFwd) {
                 // one slab per slot assignment: scalar loads, coalesced over the wave
                 // slab base uniform (SGPRs), lane offset 32-bit (planner: kChainLo32)
                 const int64_t w0 = readfirstlane64(in_off);
@@ -305,20 +322,22 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
             static_for<F>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 if (!((c.gmask >> j) & 1))                     // uniform
-                    chain_step<T, K, F, V, j, 0, DEP>(t, small, gb[j], c.gs[j], c.gsn[j]);
+                    chain_step<T, K, F, V, j, 0, DEP, SUM>(t, small, gb[j], c.gs[j], c.gsn[j]);
                 else                       // V > 1: G_j constant along the V entries (planner-checked)
-                    chain_step<T, K, F, V, j, 1, DEP>(t, small, gb[j], c.gs[j], c.gsn[j]);
+                    chain_step<T, K, F, V, j, 1, DEP, SUM>(t, small, gb[j], c.gs[j], c.gsn[j]);
             });
+            constexpr int NOUT = SUM ? 1 : N;                   // live entries (summing run: t[0])
             if (c.flags & kScale) {
 #pragma unroll
-                for (int a = 0; a < N; ++a)
+                for (int a = 0; a < NOUT; ++a)
 #pragma unroll
                     for (int v = 0; v < V; ++v) t[a][v] = ldexp_t(t[a][v], c.neg_e);
             }
 #pragma unroll
-            for (int a = 0; a < N; ++a)
+            for (int a = 0; a < NOUT; ++a)
 #pragma unroll
                 for (int v = 0; v < V; ++v) lmax = t[a][v] > lmax ? t[a][v] : lmax;
+            if constexpr (SUM) store_n<T, V, kNtStore, true>(static_cast<T *>(c.out) + out_off, t[0]);
             if constexpr (FORM == kChainBwd) {
                 T *out = static_cast<T *>(c.out);
                 const int64_t w0 = readfirstlane64(out_off);       // planner: kChainLo32
@@ -366,11 +385,13 @@ static hipError_t go_chain_level(const LevelArgs &a, int small_elems, int max_gr
     BNPP_CHAIN_ND(X, T, 4, 2, 1) X(T, 2, 2, 1, 2) X(T, 2, 3, 1, 2) X(T, 2, 4, 1, 2) X(T, 4, 2, 1, 2) \
     BNPP_CHAIN_ND(X, T, 2, 2, 2) BNPP_CHAIN_ND(X, T, 2, 3, 2) BNPP_CHAIN_ND(X, T, 2, 4, 2) BNPP_CHAIN_ND(X, T, 2, 5, 2) \
     BNPP_CHAIN_ND(X, T, 2, 6, 2) BNPP_CHAIN_ND(X, T, 4, 2, 2) BNPP_CHAIN_ND(X, T, 4, 3, 2) \
-    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) X(T, 2, 4, 2, 2) X(T, 4, 2, 2, 2)
+    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) X(T, 2, 4, 2, 2) X(T, 4, 2, 2, 2) BNPP_CHAIN_SUM(X, T)
+#define BNPP_CHAIN_SUM(X, T) X(T, 2, 2, 3, 0) X(T, 2, 3, 3, 0) X(T, 2, 4, 3, 0) X(T, 4, 2, 3, 0) \
+    X(T, 2, 2, 3, 2) X(T, 2, 3, 3, 2) X(T, 2, 4, 3, 2) X(T, 4, 2, 3, 2)
 #define BNPP_CHAIN_F64(X, T) \
     BNPP_CHAIN_ND(X, T, 2, 2, 1) BNPP_CHAIN_ND(X, T, 2, 3, 1) BNPP_CHAIN_ND(X, T, 2, 4, 1) \
     X(T, 2, 2, 1, 2) X(T, 2, 3, 1, 2) \
     BNPP_CHAIN_ND(X, T, 2, 2, 2) BNPP_CHAIN_ND(X, T, 2, 3, 2) BNPP_CHAIN_ND(X, T, 2, 4, 2) BNPP_CHAIN_ND(X, T, 2, 5, 2) \
-    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2)
+    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) BNPP_CHAIN_SUM(X, T)
 
 }  // namespace bnpp

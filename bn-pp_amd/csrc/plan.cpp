@@ -127,9 +127,11 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     if (F < 1 || (int)b.chain_n.size() != F || b.in.empty()) return fail("chain: bad run");
     const int K = cards[b.chain_x[0]];
     const int eb = max_vec == 2 ? 8 : 4;
+    const bool sum = b.chain_n[0] < 0;                // every bucket only sums (no new variable)
     int N = 1;
     for (int j = 0; j < F; ++j) {
-        if (cards[b.chain_x[j]] != K || cards[b.chain_n[j]] != K) return fail("chain: mixed cardinalities");
+        if ((b.chain_n[j] < 0) != sum) return fail("chain: mixed summing and swapping buckets");
+        if (cards[b.chain_x[j]] != K || (!sum && cards[b.chain_n[j]] != K)) return fail("chain: mixed cardinalities");
         N *= K;
     }
     if (N > 64 || (K != 2 && K != 4)) return fail("chain: register table too large");
@@ -153,7 +155,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     std::vector<int64_t> is(F), os(F);
     for (int p = 0; p < F; ++p) {
         is[p] = stride_of(big, b.chain_x[p]);
-        os[p] = out_stride(b.chain_n[p]);
+        os[p] = sum ? 0 : out_stride(b.chain_n[p]);
         if (is[p] <= 0 || os[p] < 0) return fail("chain: slot variable missing");
     }
     // rest dims (fastest first by output stride): in, out, G_j strides
@@ -185,7 +187,19 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     for (const RDim &r : md) rest *= (int64_t)r.card;
     // kernel form
     int form = 0, V = 1;
-    {
+    if (sum) {
+        // summing run: the thread's V rest entries are contiguous in the input
+        // (vector loads, one per slot assignment) and in the output
+        V = 16 / eb;
+        const int64_t W = V;
+        bool ok = !md.empty() && md[0].in == 1 && md[0].out == 1 && md[0].card % (uint64_t)V == 0 &&
+                  big.base % W == 0 && rest >= 256 * V;
+        for (const RDim &r : md) ok = ok && (r.in % W == 0 || &r == &md[0]) && (r.out % W == 0 || &r == &md[0]);
+        for (int p = 0; ok && p < F; ++p) ok = is[p] % W == 0;
+        for (int j = 0; ok && j < F; ++j) ok = md[0].g[j] == 0;
+        if (!ok) return fail("chain: summing run layout fits no kernel form");
+        form = kChainSum;
+    } else {
         bool fwd = N * eb <= 128;
         for (int p = 0; fwd && p < F; ++p) {
             int64_t pl = 1;
@@ -216,7 +230,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
             for (int p = 0; p < F; ++p) {
                 if (p == j) continue;
                 const int var = p < j ? b.chain_n[p] : b.chain_x[p];
-                if (stride_of(b.in[gidx[j]], var) == 0) continue;
+                if (var < 0 || stride_of(b.in[gidx[j]], var) == 0) continue;
                 if (p != j + 1) next = false;
                 if (p != j - 1) prev = false;
             }
@@ -240,7 +254,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         // the streamed side linear in the thread index: a wave spans 64 * V
         // consecutive rest entries -> uniform base + 32-bit lane byte offset
         bool lin = !md.empty();
-        const bool fwdf = form == kChainFwd;
+        const bool fwdf = form == kChainFwd || form == kChainSum;
         int64_t s0 = md.empty() ? 0 : (fwdf ? md[0].in : md[0].out);
         for (size_t q = 0; lin && q + 1 < md.size(); ++q) {
             const int64_t a = fwdf ? md[q].in : md[q].out, nb = fwdf ? md[q + 1].in : md[q + 1].out;
@@ -294,9 +308,9 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         const View *g = gidx[j] >= 0 ? &b.in[gidx[j]] : nullptr;
         for (int p = 0; p < F; ++p) {
             const int var = p < j ? b.chain_n[p] : b.chain_x[p];
-            pool.push_back(g ? stride_of(*g, var) : 0);
+            pool.push_back(g && var >= 0 ? stride_of(*g, var) : 0);
         }
-        pool.push_back(g ? stride_of(*g, b.chain_n[j]) : 0);
+        pool.push_back(g && b.chain_n[j] >= 0 ? stride_of(*g, b.chain_n[j]) : 0);
     }
     return true;
 }
@@ -679,12 +693,15 @@ struct PlanBuilder {
             std::vector<int> nw;
             for (int w : u)
                 if (!contains(vars, w)) nw.push_back(w);
-            if (nw.size() != 1 || nw[0] == st.x) {
+            // every bucket swaps one variable, or every bucket only sums one out
+            const bool swap_ok = nw.size() == 1 && nw[0] != st.x && (ns.empty() || ns[0] >= 0);
+            const bool sum_ok = nw.empty() && (ns.empty() || ns[0] < 0);
+            if (!swap_ok && !sum_ok) {
                 if (dbg) std::fprintf(stderr, "[chain] F=%d: bucket brings %zu new variables\n", F, nw.size());
                 return -1;
             }
             xs.push_back(st.x);
-            ns.push_back(nw[0]);
+            ns.push_back(sum_ok ? -1 : nw[0]);
             vars = remove_var(u, st.x);
         }
         BucketSpec b;
@@ -739,8 +756,13 @@ struct PlanBuilder {
         b.level = lv + 1;
         last_level = std::max(last_level, b.level);
         level[b.out_table] = b.level;
-        const double rest = (double)table_size(b.out_vars, cards) / std::pow((double)cards[xs[0]], F);
-        p.entries += F * rest * std::pow((double)cards[xs[0]], F + 1);
+        if (ns[0] >= 0) {
+            const double rest = (double)table_size(b.out_vars, cards) / std::pow((double)cards[xs[0]], F);
+            p.entries += F * rest * std::pow((double)cards[xs[0]], F + 1);
+        } else {                                        // bucket j of a summing run: rest * K^(F-j)
+            const double rest = (double)table_size(b.out_vars, cards);
+            for (int j = 0; j < F; ++j) p.entries += rest * std::pow((double)cards[xs[0]], F - j);
+        }
         p.elems_moved += moved + (double)p.msgs[b.out_table - p.n_src].size;
         p.width = std::max(p.width, (int)b.out_vars.size());
         p.buckets.push_back(b);
@@ -864,6 +886,7 @@ VEPlan plan_ve(const std::vector<int> &cards, const std::vector<View> &sources, 
             int n_msg = 0;
             for (const View &v : buckets[i]) n_msg += is_msg(v);
             for (int F = chain_first_try(nord - i); F >= 2 && n_msg == 1 && !fused; --F) {
+                    if ((nord - i) - F == 1 && F > 2) continue;   // never strand one bucket
                 const View big = buckets[i].back();
                 std::vector<PlanBuilder::ChainStep> steps;
                 std::vector<int> vars = big.vars;
@@ -1169,6 +1192,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 // longest fusable run of backward buckets jj, jj-1, ... (chain.cuh)
                 int fused = 0;
                 for (int F = chain_first_try(jj - j + 1); F >= 2 && have_pi && !fused; --F) {
+                    if ((jj - j + 1) - F == 1 && F > 2) continue;   // never strand one bucket
                     std::vector<PlanBuilder::ChainStep> steps;
                     std::vector<int> vars = pi_cur.vars;
                     for (int i = 0; i < F; ++i) {
@@ -1240,6 +1264,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 // longest fusable run of forward buckets k, k+1, ... (chain.cuh)
                 int fused = 0;
                 for (int F = chain_first_try(to - k + 1); F >= 2 && !fused; --F) {
+                    if ((to - k + 1) - F == 1 && F > 2) continue;   // never strand one bucket
                     std::vector<PlanBuilder::ChainStep> steps;
                     for (int i = 0; i < F; ++i) steps.push_back({src_in[path[k + i]], order[path[k + i]]});
                     const int t = B.emit_chain(cur, steps);

@@ -243,3 +243,24 @@ def test_partition_fused_sweep_matches_oracle(ctx, shape):
     rz, _ = refcpu.Model.from_dict(d).partition({}, "mf")      # oracle: min-fill order, fp64
     assert abs(lz - math.log10(rz)) < 1e-12 * abs(lz)
     assert abs(lz32 - lz) < 1e-6 * abs(lz)
+
+
+@pytest.mark.parametrize("spec", [(2, 14, 5), (4, 7, 4)])
+def test_summing_runs_identical_to_unfused(ctx, spec):
+    """The last column of a tall sweep only sums variables out (kChainSum runs):
+    partition and tree marginals bit-identical to one bucket per launch."""
+    k, r, c = spec
+    d = synth.ising_grid(r, c, seed=8) if k == 2 else synth.potts_grid(r, c, k=k, seed=8)
+    m = bnpp.Model.from_dict(d)
+    col = [i * c + j for j in range(c) for i in range(r)]
+    res = {}
+    for nc in ("0", "1"):
+        os.environ["BNPP_NO_CHAIN"] = nc
+        os.environ["BNPP_TREE_SLOTS"] = "3"
+        try:
+            res[nc] = [bnpp.partition(ctx, m, {}, "mf", dt, order=col)[0] for dt in (bnpp.F64, bnpp.F32)]
+            res[nc] += [bnpp.marginals_tree(ctx, m, {}, "mf", dt, order=col)[0] for dt in (bnpp.F64, bnpp.F32)]
+        finally:
+            del os.environ["BNPP_NO_CHAIN"]
+            del os.environ["BNPP_TREE_SLOTS"]
+    assert res["0"] == res["1"]

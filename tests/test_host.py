@@ -216,3 +216,18 @@ def test_plan_fused_sweep_cuts_traffic():
     assert fused[4] == plain[4] == 32
     assert abs(fused[0] - plain[0]) < 0.01 * plain[0]
     assert fused[6] * 3 < plain[6]
+
+
+def test_plan_uses_summing_runs():
+    """A tall column sweep ends in a column whose buckets only sum: the plan
+    fuses them (kChainSum): less traffic than with fusion disabled."""
+    from bnpp import synth
+    m = bnpp.Model.from_dict(synth.ising_grid(14, 5, seed=8))
+    col = [i * 5 + j for j in range(5) for i in range(14)]
+    fused = bnpp.plan_stats(m, 0, {}, "mf", dtype=bnpp.F32, order=col)
+    os.environ["BNPP_NO_CHAIN"] = "1"
+    try:
+        plain = bnpp.plan_stats(m, 0, {}, "mf", dtype=bnpp.F32, order=col)
+    finally:
+        del os.environ["BNPP_NO_CHAIN"]
+    assert fused[6] < 0.6 * plain[6]
