@@ -107,7 +107,10 @@ __host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 409
 //   kChainSum: every bucket only sums its variable out (no new variable: the
 //              last column of a sweep); slots are the input's slabs, V rest
 //              entries per thread contiguous in input and output
-enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2, kChainSum = 3 };
+//   kChainFwdV: kChainFwd with V rest entries per thread (vector slab loads,
+//              rows of V * K^F entries); short runs, where one entry per
+//              thread leaves the kernel issue-bound
+enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2, kChainSum = 3, kChainFwdV = 4 };
 // Which slots G_j depends on besides its own (x_j, n_j): the next slot (j+1,
 // e.g. a forward sweep's vertical factor), the previous one (j-1, backward),
 // or any (every G value of a bucket fetched separately; small tables only).
@@ -118,6 +121,11 @@ __host__ __device__ inline int chain_key(int form, int k, int f, int dep) {
 // rest entries per thread of the backward form (the forward form has 1)
 __host__ __device__ constexpr int chain_bwd_v(int n, int elem_bytes) {
     return 64 / n < 1 ? 1 : (64 / n > 16 / elem_bytes ? 16 / elem_bytes : 64 / n);
+}
+// rest entries per thread of kChainFwdV: 16 B loads, rows of at most 128 B
+__host__ __device__ constexpr int chain_fwd_v(int n, int elem_bytes) {
+    return n * elem_bytes * (16 / elem_bytes) <= 128 ? 16 / elem_bytes
+           : n * elem_bytes * (8 / elem_bytes) <= 128 && elem_bytes <= 4 ? 8 / elem_bytes : 1;
 }
 // chain pool rows: per rest dim (fastest first) 4 + F words
 //   w0 header  w1 magic  w2 input stride  w3 output stride  w4.. G_j stride (j < F)

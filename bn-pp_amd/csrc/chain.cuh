@@ -205,9 +205,17 @@ __device__ __forceinline__ void chain_step(T (&t)[ipow(K, F)][V], const T *small
     });
 }
 
-// per-wave LDS image of the forward form: 64 rows of K^F entries (+16 B pad)
-template <typename T, int K, int F>
-constexpr int chain_img_wave() { return 64 * (ipow(K, F) * (int)sizeof(T) + kLdsRowPad); }
+__host__ __device__ constexpr bool chain_fwd(int form) { return form == kChainFwd || form == kChainFwdV; }
+// rest entries per thread
+template <typename T, int K, int F, int FORM>
+constexpr int chain_v() {
+    return FORM == kChainFwd ? 1
+           : FORM == kChainFwdV ? chain_fwd_v(ipow(K, F), (int)sizeof(T))
+           : FORM == kChainSum ? 16 / (int)sizeof(T) : chain_bwd_v(ipow(K, F), (int)sizeof(T));
+}
+// per-wave LDS image of the forward forms: 64 rows of V * K^F entries (+16 B pad)
+template <typename T, int K, int F, int FORM>
+constexpr int chain_img_wave() { return 64 * (chain_v<T, K, F, FORM>() * ipow(K, F) * (int)sizeof(T) + kLdsRowPad); }
 
 // waves per SIMD the register allocation must leave room for (0: compiler's
 // choice).  Measured on the 32x32 sweep: the forward 32-entry run at 3 waves
@@ -226,12 +234,13 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
     using S = ChainShape<K, F>;
     constexpr int N = S::N;
     constexpr bool SUM = FORM == kChainSum;
-    constexpr int V = FORM == kChainFwd ? 1 : SUM ? 16 / (int)sizeof(T) : chain_bwd_v(N, (int)sizeof(T));
-    static_assert(FORM != kChainFwd || N * (int)sizeof(T) <= 128, "forward rows go through the wave's LDS image");
+    constexpr bool FWD = chain_fwd(FORM);
+    constexpr int V = chain_v<T, K, F, FORM>();
+    static_assert(!FWD || V * N * (int)sizeof(T) <= 128, "forward rows go through the wave's LDS image");
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
     unsigned char *stage = dyn + kRedBytes;
-    constexpr int kImg = FORM == kChainFwd ? (kBlock / 64) * chain_img_wave<T, K, F>() : 0;
+    constexpr int kImg = FWD ? (kBlock / 64) * chain_img_wave<T, K, F, FORM>() : 0;
     T *small = reinterpret_cast<T *>(dyn + kRedBytes + kImg);
 
     ChainState<F> c;
@@ -295,8 +304,8 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                     for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.is[p];
                     load_n<T, V, kNtLoad, true>(reinterpret_cast<const T *>(wb + o * (int64_t)sizeof(T) + lob), t[a]);
                 }
-            } else if constexpr (FORM == kChainFwd) {
-                // one slab per slot assignment: scalar loads, coalesced over the wave
+            } else if constexpr (FWD) {
+                // one slab per slot assignment: V-wide loads, coalesced over the wave
                 // slab base uniform (SGPRs), lane offset 32-bit (planner: kChainLo32)
                 const int64_t w0 = readfirstlane64(in_off);
                 const uint32_t lob = (uint32_t)((in_off - w0) * (int64_t)sizeof(T));
@@ -306,7 +315,10 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                     int64_t o = 0;
 #pragma unroll
                     for (int p = 0; p < F; ++p) o += (int64_t)S::digit(a, p) * c.is[p];
-                    t[a][0] = gload(reinterpret_cast<const T *>(wb + o * (int64_t)sizeof(T) + lob));
+                    if constexpr (V == 1)
+                        t[a][0] = gload(reinterpret_cast<const T *>(wb + o * (int64_t)sizeof(T) + lob));
+                    else
+                        load_n<T, V, kNtLoad, true>(reinterpret_cast<const T *>(wb + o * (int64_t)sizeof(T) + lob), t[a]);
                 }
             } else {
                 // K^F contiguous entries (slot 0 fastest) per rest entry
@@ -352,13 +364,15 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                 }
             }
         }
-        if constexpr (FORM == kChainFwd) {
-            // the thread's K^F outputs are the contiguous row tid (planner-checked)
-            T row[N];
+        if constexpr (FWD) {
+            // the thread's V * K^F outputs are the contiguous row tid (planner-checked)
+            T row[V * N];
 #pragma unroll
-            for (int a = 0; a < N; ++a) row[a] = t[a][0];
-            store_tiles<T, N>(static_cast<T *>(c.out), tid0 + (threadIdx.x & ~63), c.n_tiles, row,
-                              stage + (threadIdx.x >> 6) * chain_img_wave<T, K, F>());
+            for (int v = 0; v < V; ++v)
+#pragma unroll
+                for (int a = 0; a < N; ++a) row[v * N + a] = t[a][v];
+            store_tiles<T, V * N>(static_cast<T *>(c.out), tid0 + (threadIdx.x & ~63), c.n_tiles, row,
+                                  stage + (threadIdx.x >> 6) * chain_img_wave<T, K, F, FORM>());
         }
     }
     if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
@@ -367,7 +381,7 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
 template <typename T, int K, int F, int FORM, int DEP>
 static hipError_t go_chain_level(const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream) {
     const int64_t grid = a.vblocks < max_grid ? a.vblocks : max_grid;
-    const size_t img = FORM == kChainFwd ? (size_t)(kBlock / 64) * chain_img_wave<T, K, F>() : 0;
+    const size_t img = chain_fwd(FORM) ? (size_t)(kBlock / 64) * chain_img_wave<T, K, F, FORM>() : 0;
     const size_t shm = kRedBytes + img + (size_t)small_elems * sizeof(T);
     hipLaunchKernelGGL((chain_level_kernel<T, K, F, FORM, DEP>), dim3((unsigned)grid), dim3(kBlock), shm, stream,
                        a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
@@ -377,7 +391,8 @@ static hipError_t go_chain_level(const LevelArgs &a, int small_elems, int max_gr
 #define BNPP_CASE_CHAIN(T, K, F, FORM, DEP) \
     case 8192 + DEP * 2048 + FORM * 256 + K * 16 + F: return go_chain_level<T, K, F, FORM, DEP>(a, small_elems, max_grid, stream);
 #define BNPP_CASE_CHAIN_OK(T, K, F, FORM, DEP) case 8192 + DEP * 2048 + FORM * 256 + K * 16 + F: return true;
-// instantiated shapes: forward rows <= 128 B, backward tables <= 64 entries
+// instantiated shapes: forward rows <= 128 B (V-wide forward for runs of
+// 4..16 entries), backward tables <= 64 entries
 // (V = 1 there); dep "any" only for tables <= 16 entries
 #define BNPP_CHAIN_ND(X, T, K, F, FORM) X(T, K, F, FORM, 0) X(T, K, F, FORM, 1)
 #define BNPP_CHAIN_F32(X, T) \
@@ -385,13 +400,16 @@ static hipError_t go_chain_level(const LevelArgs &a, int small_elems, int max_gr
     BNPP_CHAIN_ND(X, T, 4, 2, 1) X(T, 2, 2, 1, 2) X(T, 2, 3, 1, 2) X(T, 2, 4, 1, 2) X(T, 4, 2, 1, 2) \
     BNPP_CHAIN_ND(X, T, 2, 2, 2) BNPP_CHAIN_ND(X, T, 2, 3, 2) BNPP_CHAIN_ND(X, T, 2, 4, 2) BNPP_CHAIN_ND(X, T, 2, 5, 2) \
     BNPP_CHAIN_ND(X, T, 2, 6, 2) BNPP_CHAIN_ND(X, T, 4, 2, 2) BNPP_CHAIN_ND(X, T, 4, 3, 2) \
-    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) X(T, 2, 4, 2, 2) X(T, 4, 2, 2, 2) BNPP_CHAIN_SUM(X, T)
+    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) X(T, 2, 4, 2, 2) X(T, 4, 2, 2, 2) BNPP_CHAIN_SUM(X, T) \
+    BNPP_CHAIN_ND(X, T, 2, 2, 4) BNPP_CHAIN_ND(X, T, 2, 3, 4) BNPP_CHAIN_ND(X, T, 2, 4, 4) BNPP_CHAIN_ND(X, T, 4, 2, 4) \
+    X(T, 2, 2, 4, 2) X(T, 2, 3, 4, 2)
 #define BNPP_CHAIN_SUM(X, T) X(T, 2, 2, 3, 0) X(T, 2, 3, 3, 0) X(T, 2, 4, 3, 0) X(T, 4, 2, 3, 0) \
     X(T, 2, 2, 3, 2) X(T, 2, 3, 3, 2) X(T, 2, 4, 3, 2) X(T, 4, 2, 3, 2)
 #define BNPP_CHAIN_F64(X, T) \
     BNPP_CHAIN_ND(X, T, 2, 2, 1) BNPP_CHAIN_ND(X, T, 2, 3, 1) BNPP_CHAIN_ND(X, T, 2, 4, 1) \
     X(T, 2, 2, 1, 2) X(T, 2, 3, 1, 2) \
     BNPP_CHAIN_ND(X, T, 2, 2, 2) BNPP_CHAIN_ND(X, T, 2, 3, 2) BNPP_CHAIN_ND(X, T, 2, 4, 2) BNPP_CHAIN_ND(X, T, 2, 5, 2) \
-    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) BNPP_CHAIN_SUM(X, T)
+    X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) BNPP_CHAIN_SUM(X, T) \
+    BNPP_CHAIN_ND(X, T, 2, 2, 4) BNPP_CHAIN_ND(X, T, 2, 3, 4) X(T, 2, 2, 4, 2) X(T, 2, 3, 4, 2)
 
 }  // namespace bnpp

@@ -187,6 +187,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     for (const RDim &r : md) rest *= (int64_t)r.card;
     // kernel form
     int form = 0, V = 1;
+    bool fwd_v = false;
     if (sum) {
         // summing run: the thread's V rest entries are contiguous in the input
         // (vector loads, one per slot assignment) and in the output
@@ -217,6 +218,14 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         for (const RDim &r : md) bwd = bwd && r.in % W == 0 && (r.out % bv == 0 || &r == &md[0]);
         for (int p = 0; bwd && p < F; ++p) bwd = os[p] % bv == 0;
         for (int j = 0; bwd && bv > 1 && j < F; ++j) bwd = md[0].g[j] == 0;   // G constant along a thread's V entries
+        // V-wide forward: the thread's V rest entries contiguous in input and
+        // output (rest dim 0 innermost in the input), G constant along them
+        const int fv = chain_fwd_v(N, eb);
+        fwd_v = fwd && fv > 1 && !md.empty() && md[0].in == 1 && md[0].card % (uint64_t)fv == 0 &&
+                big.base % fv == 0 && rest >= 256 * fv;
+        for (const RDim &r : md) fwd_v = fwd_v && (r.in % fv == 0 || &r == &md[0]);
+        for (int p = 0; fwd_v && p < F; ++p) fwd_v = is[p] % fv == 0;
+        for (int j = 0; fwd_v && j < F; ++j) fwd_v = md[0].g[j] == 0;
         if (fwd) form = kChainFwd;
         else if (bwd) { form = kChainBwd; V = bv; }
         else return fail("chain: layout fits no kernel form");
@@ -237,7 +246,13 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         }
         dep = next ? kDepNext : prev ? kDepPrev : kDepAny;
     }
+    if (fwd_v && !std::getenv("BNPP_NO_CHAIN_FWDV") && chain_supported(eb, chain_key(kChainFwdV, K, F, dep))) {
+        form = kChainFwdV;
+        V = chain_fwd_v(N, eb);
+    }
     if (!chain_supported(eb, chain_key(form, K, F, dep))) return fail("chain: shape not instantiated");
+    if (std::getenv("BNPP_DEBUG_CHAIN"))
+        std::fprintf(stderr, "[chain] run form %d K=%d F=%d dep %d V=%d rest %lld\n", form, K, F, dep, V, (long long)rest);
     d = BucketDesc{};
     d.out_size = rest * N;
     d.n_tiles = rest / V;
@@ -254,7 +269,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         // the streamed side linear in the thread index: a wave spans 64 * V
         // consecutive rest entries -> uniform base + 32-bit lane byte offset
         bool lin = !md.empty();
-        const bool fwdf = form == kChainFwd || form == kChainSum;
+        const bool fwdf = form == kChainFwd || form == kChainFwdV || form == kChainSum;
         int64_t s0 = md.empty() ? 0 : (fwdf ? md[0].in : md[0].out);
         for (size_t q = 0; lin && q + 1 < md.size(); ++q) {
             const int64_t a = fwdf ? md[q].in : md[q].out, nb = fwdf ? md[q + 1].in : md[q + 1].out;
@@ -569,9 +584,18 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
 
 // ---------------------------------------------------------------- VE plan
 constexpr int kChainRunMax = 6;                   // longest fused run tried (fp32, K = 2, backward)
+// BNPP_CHAIN_RUN_MAX (tests): a shorter cap, to exercise the short-run kernels
+inline int chain_run_max() {
+    const char *e = std::getenv("BNPP_CHAIN_RUN_MAX");
+    const int v = e ? std::atoi(e) : kChainRunMax;
+    return v >= 2 && v <= kChainRunMax ? v : kChainRunMax;
+}
 // first run length to try for `rem` remaining buckets: never leave a single
 // bucket behind when a split into runs >= 2 exists (5 -> 3 + 2, not 4 + 1)
-inline int chain_first_try(int rem) { return rem == kChainRunMax + 1 ? kChainRunMax - 1 : std::min(kChainRunMax, rem); }
+inline int chain_first_try(int rem) {
+    const int mx = chain_run_max();
+    return rem == mx + 1 && mx > 2 ? mx - 1 : std::min(mx, rem);
+}
 
 namespace {
 // Emits buckets and message tables into a VEPlan (shared by plan_ve and

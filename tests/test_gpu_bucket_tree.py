@@ -264,3 +264,29 @@ def test_summing_runs_identical_to_unfused(ctx, spec):
             del os.environ["BNPP_NO_CHAIN"]
             del os.environ["BNPP_TREE_SLOTS"]
     assert res["0"] == res["1"]
+
+
+@pytest.mark.parametrize("spec", [(2, 16, 5), (4, 8, 4)])
+def test_short_forward_runs_vector_form(ctx, spec):
+    """Short forward runs (2..4 buckets) take the V-wide forward form
+    (kChainFwdV, several rest entries per thread): partition and tree marginals
+    bit-identical to the one-entry form and to one bucket per launch."""
+    k, r, c = spec
+    d = synth.ising_grid(r, c, seed=11) if k == 2 else synth.potts_grid(r, c, k=k, seed=11)
+    m = bnpp.Model.from_dict(d)
+    col = [i * c + j for j in range(c) for i in range(r)]
+    knobs = [{"BNPP_CHAIN_RUN_MAX": str(rm)} for rm in (2, 3, 4)]
+    knobs += [dict(kn, BNPP_NO_CHAIN_FWDV="1") for kn in knobs] + [{"BNPP_NO_CHAIN": "1"}]
+    res = []
+    for kn in knobs:
+        os.environ.update(kn)
+        os.environ["BNPP_TREE_SLOTS"] = "3"
+        try:
+            out = [bnpp.partition(ctx, m, {}, "mf", dt, order=col)[0] for dt in (bnpp.F64, bnpp.F32)]
+            out += [bnpp.marginals_tree(ctx, m, {}, "mf", dt, order=col)[0] for dt in (bnpp.F64, bnpp.F32)]
+            res.append(out)
+        finally:
+            for key in list(kn) + ["BNPP_TREE_SLOTS"]:
+                del os.environ[key]
+    for out in res[1:]:
+        assert out == res[0]
