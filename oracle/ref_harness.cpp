@@ -15,6 +15,7 @@
 //   width <uai> <mf|wmf|md>                    Graph::ordering induced width
 //   kat   <opfile>                             single Factor ops (product, sum_out, ...)
 //   micro <k> <w> <reps>                       m(x,S)*f(x,y) -> sum_x, timed
+//   sp    <uai> [max] [eps]                    loopy BP (FactorGraph, graph.cpp:256-403)
 #include "variable.hh"
 #include "domain.hh"
 #include "factor.hh"
@@ -201,6 +202,30 @@ int main(int argc, char **argv) {
         }
         for (auto &kv : fs) delete kv.second;
         for (auto &kv : vars) delete kv.second;
+        return 0;
+    }
+    if (cmd == "sp" && argc >= 3) {
+        // loopy BP as BN::sum_product (model.cpp:736-753) + marginals
+        // (model.cpp:313-317); the iteration count FactorGraph::update returns
+        BN *m = load(argv[2]);
+        const unsigned max_it = argc >= 4 ? (unsigned)std::atoi(argv[3]) : 10000;
+        const double eps = argc >= 5 ? std::atof(argv[4]) : 0.001;
+        std::vector<const Variable *> mv(m->variables().begin(), m->variables().end());
+        std::vector<const Factor *> fs(m->factors().begin(), m->factors().end());
+        auto t0 = std::chrono::steady_clock::now();
+        FactorGraph g(mv, fs);
+        const unsigned it = g.update(max_it, eps);
+        std::vector<Factor> marg;
+        for (auto pv : mv) marg.push_back(g.marginal(pv));
+        auto t1 = std::chrono::steady_clock::now();
+        std::printf("iterations %u\n", it);
+        for (size_t i = 0; i < marg.size(); ++i) {
+            char tag[32];
+            std::snprintf(tag, sizeof tag, "M%u", mv[i]->id());
+            print_factor(tag, marg[i]);
+        }
+        std::printf("uptime_ms %.6f\n", std::chrono::duration<double, std::milli>(t1 - t0).count());
+        delete m;
         return 0;
     }
     if (cmd == "micro" && argc >= 5) {

@@ -712,3 +712,108 @@ double rc_micro_bucket(int k, int w, int reps, double *seconds_out) {
     if (sink < 0) fprintf(stderr, "impossible\n");
     return entries * reps / sec;
 }
+
+/* ------------------------------------------------------ loopy BP (-sp) */
+/* FactorGraph (graph.cpp:256-403) as driven by BN::sum_product + marginals
+   (model.cpp:313-317, 736-753): flooding schedule, every variable->factor
+   message, then every factor->variable message, convergence on the largest
+   relative change |old - new| / old of the iteration (graph.cpp:298-332).
+   Restated with this file's factor algebra.  Deviation: the reference walks
+   unordered_maps keyed by id (graph.hh:50-51), so its products run in hash
+   order; here they run by ascending factor id (variable side) and in scope
+   order (factor side) -- the same values up to rounding. */
+static double sp_replace(rc_factor **slot, rc_factor *raw) {
+    rc_factor *nw = rc_normalize(raw);                               /* graph.cpp:345, 374 */
+    rc_factor_free(raw);
+    const rc_factor *old = *slot;
+    double maxerror = 0.0;
+    for (uint64_t i = 0; i < old->size; ++i) {                        /* graph.cpp:348-356 */
+        double err = fabs(old->values[i] - nw->values[i]) / old->values[i];
+        if (err > maxerror) maxerror = err;
+    }
+    rc_factor_free(*slot);
+    *slot = nw;
+    return maxerror;
+}
+
+int rc_sum_product(const rc_model *m, int max_iter, double eps, double *out, int *iterations, double *uptime_ms) {
+    double t0 = now_ms();
+    int n_edges = 0;
+    for (int f = 0; f < m->n_factors; ++f) n_edges += m->factors[f]->width;
+    int *e_off = (int *)xmalloc(sizeof(int) * (size_t)(m->n_factors + 1));
+    rc_factor **v2f = (rc_factor **)xcalloc((size_t)n_edges, sizeof(rc_factor *));
+    rc_factor **f2v = (rc_factor **)xcalloc((size_t)n_edges, sizeof(rc_factor *));
+    e_off[0] = 0;
+    for (int f = 0; f < m->n_factors; ++f) {
+        const rc_factor *F = m->factors[f];
+        e_off[f + 1] = e_off[f] + F->width;
+        for (int j = 0; j < F->width; ++j) {                          /* graph.cpp:265-273 */
+            int v = F->vars[j], r = F->cards[j];
+            double *u = (double *)xmalloc(sizeof(double) * (size_t)r);
+            for (int x = 0; x < r; ++x) u[x] = 1.0 / r;
+            f2v[e_off[f] + j] = rc_factor_new(1, &v, &r, u);
+            v2f[e_off[f] + j] = rc_factor_new(1, &v, &r, u);
+            free(u);
+        }
+    }
+    int it;
+    for (it = 0; it < max_iter; ++it) {
+        double maxerror = 0.0;
+        for (int f = 0; f < m->n_factors; ++f)                        /* graph.cpp:306-315 */
+            for (int j = 0; j < m->factors[f]->width; ++j) {
+                int v = m->factors[f]->vars[j], r = m->factors[f]->cards[j];
+                rc_factor *nw = rc_factor_new(1, &v, &r, NULL);       /* Factor(sc, 1.0), graph.cpp:339 */
+                for (uint64_t x = 0; x < nw->size; ++x) nw->values[x] = 1.0;
+                nw->partition = (double)r;                            /* factor.cpp:18-23 */
+                for (int g = 0; g < m->n_factors; ++g) {
+                    if (g == f) continue;
+                    for (int k = 0; k < m->factors[g]->width; ++k)
+                        if (m->factors[g]->vars[k] == v) {
+                            rc_factor *p = rc_product(nw, f2v[e_off[g] + k]);
+                            rc_factor_free(nw);
+                            nw = p;
+                        }
+                }
+                double err = sp_replace(&v2f[e_off[f] + j], nw);
+                if (err > maxerror) maxerror = err;
+            }
+        for (int f = 0; f < m->n_factors; ++f)                        /* graph.cpp:317-326 */
+            for (int j = 0; j < m->factors[f]->width; ++j) {
+                const rc_factor *F = m->factors[f];
+                rc_factor *nw = rc_factor_copy(F);                    /* graph.cpp:367-373 */
+                for (int k = 0; k < F->width; ++k) {
+                    if (k == j) continue;
+                    rc_factor *p = rc_product(nw, v2f[e_off[f] + k]);
+                    rc_factor_free(nw);
+                    nw = rc_sum_out(p, F->vars[k], F->cards[k]);
+                    rc_factor_free(p);
+                }
+                double err = sp_replace(&f2v[e_off[f] + j], nw);
+                if (err > maxerror) maxerror = err;
+            }
+        if (maxerror < eps) break;                                    /* graph.cpp:328 */
+    }
+    /* FactorGraph::marginal (graph.cpp:393-403), var-major output */
+    size_t o = 0;
+    for (int v = 0; v < m->n_vars; ++v) {
+        rc_factor *mg = rc_factor_new(0, NULL, NULL, NULL);
+        mg->values[0] = 1.0;
+        mg->partition = 1.0;
+        for (int g = 0; g < m->n_factors; ++g)
+            for (int k = 0; k < m->factors[g]->width; ++k)
+                if (m->factors[g]->vars[k] == v) {
+                    rc_factor *p = rc_product(mg, f2v[e_off[g] + k]);
+                    rc_factor_free(mg);
+                    mg = p;
+                }
+        rc_factor *nm = rc_normalize(mg);
+        for (int x = 0; x < m->cards[v]; ++x) out[o++] = nm->size == (uint64_t)m->cards[v] ? nm->values[x] : 1.0 / m->cards[v];
+        rc_factor_free(mg);
+        rc_factor_free(nm);
+    }
+    for (int e = 0; e < n_edges; ++e) { rc_factor_free(v2f[e]); rc_factor_free(f2v[e]); }
+    free(v2f); free(f2v); free(e_off);
+    if (iterations) *iterations = it;
+    if (uptime_ms) *uptime_ms = now_ms() - t0;
+    return 0;
+}

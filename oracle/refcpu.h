@@ -27,6 +27,7 @@
  *   PR / MAR    conditioning + VE (+ normalize)                    model.cpp:250-346
  *   ordering    min-fill / weighted-min-fill / min-degree          graph.cpp:41-195
  *   UAI I/O     token reader, '#' comments, evidence               io.cpp:14-180
+ *   loopy BP    flooding sum-product, relative-change stop         graph.cpp:256-403
  *
  * Deliberate, documented deviations (none changes a value beyond fp
  * rounding of >=3-factor chains):
@@ -113,6 +114,11 @@ int rc_marginals(const rc_model *m, int n_ev, const int *ev_vars, const int *ev_
 /* marginal of one variable (one VE of the MAR loop, model.cpp:326-334) */
 int rc_marginal_one(const rc_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
                     int heuristic, int target, double *out);
+
+/* loopy BP, BN::sum_product + FactorGraph::marginal (model.cpp:313-317,
+   736-753; graph.cpp:256-403); evidence is not used on this path.  Writes
+   sum(card) values, var-major; *iterations = FactorGraph::update's result */
+int rc_sum_product(const rc_model *m, int max_iter, double eps, double *out, int *iterations, double *uptime_ms);
 
 /* bucket micro-benchmark: m(x,S_1..S_w)*f(x,y) -> sum_x, all cards = k.
    Returns factor-entries processed per second (k^(w+2) / seconds), fp64. */

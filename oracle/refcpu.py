@@ -43,6 +43,7 @@ for name, res, args in [
     ("rc_marginals", _I, [_P, _I, _IP, _IP, _I, _DP, _DP]),
     ("rc_marginal_one", _I, [_P, _I, _IP, _IP, _I, _I, _DP]),
     ("rc_micro_bucket", C.c_double, [_I, _I, _I, _DP]),
+    ("rc_sum_product", _I, [_P, _I, C.c_double, _DP, _IP, _DP]),
     ("rc_ordering", _I, [_P, _I, C.POINTER(_P), _I, _IP, _I, _IP]),
 ]:
     f = getattr(_lib, name)
@@ -163,6 +164,17 @@ class Model:
             res[t] = list(out[o:o + self.cards[t]])
             o += self.cards[t]
         return res, up.value
+
+    def sum_product(self, max_iter: int = 10000, eps: float = 0.001):
+        """Loopy BP (model.cpp:313-317, 736-753) -> (marginals {var: [..]}, iterations, uptime_ms)."""
+        out = (C.c_double * max(sum(self.cards), 1))()
+        it, up = C.c_int(), C.c_double()
+        _lib.rc_sum_product(self.h, max_iter, eps, out, C.byref(it), C.byref(up))
+        res, o = {}, 0
+        for t in range(self.n_vars):
+            res[t] = list(out[o:o + self.cards[t]])
+            o += self.cards[t]
+        return res, it.value, up.value
 
     def ordering(self, variables: Sequence[int], heuristic: str = "mf"):
         """Graph::ordering over the model's own (unconditioned) factors -> (order, width)."""

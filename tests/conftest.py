@@ -37,6 +37,12 @@ def golden_kat():
 
 
 @pytest.fixture(scope="session")
+def golden_sp():
+    with open(os.path.join(GOLDEN, "sp_golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
 def ctx():
     import bnpp
     c = bnpp.Context(0)

@@ -3,7 +3,8 @@
 
 Run in the build container (needs /root/reference and `make -C oracle ref`):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          # everything
+    python tests/golden/make_golden.py sp       # loopy BP fixtures only (sp_golden.json)
 
 It
   1. copies the reference's own model + fixture files that the tests use into
@@ -252,5 +253,33 @@ def main():
     print("kat cases", len(cases), "outputs", len(outs))
 
 
+# loopy BP (-sp): BN::sum_product + marginals (model.cpp:313-317, 736-753);
+# evidence is ignored by the reference on this path.  (model, max_iter, eps)
+SP_CASES = [("asia.uai", 10000, 0.001), ("cancer.uai", 10000, 0.001), ("earthquake.uai", 10000, 0.001),
+            ("alarm.uai", 10000, 0.001), ("alarm.uai", 10000, 1e-9), ("child.uai", 10000, 0.001),
+            ("insurance.uai", 10000, 0.001), ("hailfinder.uai", 10000, 0.001), ("win95pts.uai", 10000, 0.001),
+            ("hepar2.uai", 10000, 0.001), ("andes.uai", 10000, 0.001), ("Water.uai", 10000, 0.001),
+            ("pathfinder.uai", 10000, 0.001), ("network.uai", 10000, 0.001), ("ising4x4.uai", 10000, 0.001),
+            ("ising8x8.uai", 10000, 0.001), ("ising10x10.uai", 10000, 1e-6), ("potts4x5k3.uai", 10000, 0.001),
+            ("noisyor_30_40.uai", 10000, 0.001), ("grid3x3.uai", 50, 0.001), ("asia.uai", 0, 0.001)]
+
+
+def sp_golden():
+    cases = []
+    for model, mx, eps in SP_CASES:
+        txt = run("sp", model_path(model), mx, repr(eps))
+        kv = parse_kv(txt)
+        marg = {int(t[1:]): f["values"] for t, f in parse_factors(txt).items()}
+        cases.append({"model": model, "max_iter": mx, "eps": eps, "iterations": int(kv["iterations"]),
+                      "marginals": marg, "ref_uptime_ms": kv.get("uptime_ms")})
+        print("sp", model, mx, eps, int(kv["iterations"]))
+    with open(os.path.join(HERE, "sp_golden.json"), "w") as f:
+        json.dump({"cases": cases}, f)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["sp"]:
+        sp_golden()
+    else:
+        main()
+        sp_golden()

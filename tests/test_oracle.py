@@ -125,3 +125,18 @@ def test_oracle_widths_close_to_reference(golden_ve):
 def test_oracle_micro_bucket_runs(k, w):
     eps, sec = refcpu.micro_bucket(k, w, 1)
     assert eps > 0 and sec >= 0
+
+
+def test_oracle_sum_product_matches_reference(golden_sp):
+    """Loopy BP (-sp): same iteration count as FactorGraph::update and the same
+    marginals up to the product order of the reference's unordered_maps
+    (graph.hh:50-51), on BNs, grids (loopy) and a non-converging 3x3 grid."""
+    for case in golden_sp["cases"]:
+        m = refcpu.Model.load(model_path(case["model"]))
+        marg, it, _ = m.sum_product(case["max_iter"], case["eps"])
+        assert it == case["iterations"], (case["model"], it, case["iterations"])
+        for t, ref in case["marginals"].items():
+            got = marg[int(t)]
+            assert len(got) == len(ref)
+            for a, b in zip(got, ref):
+                assert abs(a - b) <= 1e-12, (case["model"], t, a, b)
