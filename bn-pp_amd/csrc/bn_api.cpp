@@ -383,7 +383,11 @@ std::vector<const Factor *> Model::marginals(const std::unordered_map<unsigned, 
     for (auto pv : _variables) targets.push_back((int)pv->id());
     double up = 0;
     int dt = options["fp32"] ? BNPP_F32 : BNPP_F64;
-    if (options["bucket-tree"])                      // all marginals from one bucket tree (to rounding)
+    const bool sp = options["sum-product"];
+    if (sp) {                                        // loopy BP, evidence unused (model.cpp:313-317, 749)
+        int it = 0;
+        check(bnpp_sum_product(ctx(), g.m, 10000, 0.001, out.data(), &it, &up), "marginals (sum-product)");
+    } else if (options["bucket-tree"])               // all marginals from one bucket tree (to rounding)
         check(bnpp_marginals_tree(ctx(), g.m, (int)ev_vars.size(), ev_vars.data(), ev_vals.data(),
                                   heuristic_of(options), nullptr, 0, (int)targets.size(), targets.data(), dt,
                                   out.data(), &up),
@@ -395,7 +399,7 @@ std::vector<const Factor *> Model::marginals(const std::unordered_map<unsigned, 
     std::vector<const Factor *> marg;
     size_t o = 0;
     for (auto pv : _variables) {
-        if (evidence.count(pv->id())) {               // width-0 factor with value 1 (model.cpp:333)
+        if (!sp && evidence.count(pv->id())) {        // width-0 factor with value 1 (model.cpp:333)
             marg.push_back(new Factor(new Domain(), std::vector<double>{1.0}, 1.0));
         } else {
             std::vector<double> v(out.begin() + o, out.begin() + o + pv->size());

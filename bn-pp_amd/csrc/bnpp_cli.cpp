@@ -20,6 +20,7 @@ int main(int argc, char **argv) {
         else if (p == "-mar") options["marginals"] = true;
         else if (p == "-mar-tree") { options["marginals"] = true; options["bucket-tree"] = true; }
         else if (p == "-ve") options["variable-elimination"] = true;
+        else if (p == "-sp") options["sum-product"] = true;      // bn.cpp:177-178: loopy BP marginals
         else if (p == "-mf") options["min-fill"] = true;
         else if (p == "-wmf") options["weighted-min-fill"] = true;
         else if (p == "-md") options["min-degree"] = true;
@@ -30,7 +31,7 @@ int main(int argc, char **argv) {
         else positional.push_back(p);
     }
     if (positional.empty() || options["help"]) {
-        std::cout << "usage: " << argv[0] << " /path/to/model.uai [/path/to/evidence.uai.evid] -pr|-mar|-mar-tree [-mf|-wmf|-md] [-f32]" << std::endl;
+        std::cout << "usage: " << argv[0] << " /path/to/model.uai [/path/to/evidence.uai.evid] -pr|-mar|-mar-tree [-sp] [-mf|-wmf|-md] [-f32]" << std::endl;
         return positional.empty() ? 1 : 0;
     }
     bnpp_model *probe = nullptr;

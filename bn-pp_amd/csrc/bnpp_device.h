@@ -139,4 +139,28 @@ inline int64_t pack_dim_header(uint32_t card, uint32_t shift, bool pow2) {
     return (int64_t)((uint64_t)card | ((uint64_t)shift << 32) | ((uint64_t)(pow2 ? 1 : 0) << 40));
 }
 
+// Loopy BP over the factor graph (bp.hip; graph.cpp:256-403).  Edge e joins
+// factor edge_fac[e] and its scope variable edge_var[e]; a factor's edges are
+// [f_edge_off[f], f_edge_off[f+1]) in scope order, a variable's are
+// v_edges[v_edge_off[v] .. v_edge_off[v+1]) by ascending factor id.  Message e
+// occupies [msg_off[e], msg_off[e+1]) of v2f / f2v / raw; item_edge maps a
+// message entry back to its edge.  edge_stride[e]: stride of edge_var[e] in
+// the factor's table (row-major, last scope variable fastest).
+struct BpArgs {
+    int32_t n_vars, n_edges, n_msg, max_iter;
+    double eps;
+    const int32_t *cards;
+    const double *tables;
+    const int64_t *tab_off;                 // n_factors + 1
+    const int32_t *f_edge_off;              // n_factors + 1
+    const int32_t *edge_var, *edge_fac;     // n_edges
+    const uint32_t *edge_stride;            // n_edges
+    const int32_t *msg_off;                 // n_edges + 1
+    const int32_t *item_edge;               // n_msg
+    const int32_t *v_edge_off, *v_edges;    // n_vars + 1, n_edges
+    const int32_t *marg_off;                // n_vars + 1
+    double *v2f, *f2v, *raw, *marg;
+    int32_t *iterations;
+};
+
 }  // namespace bnpp

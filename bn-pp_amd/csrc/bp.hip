@@ -1,0 +1,136 @@
+// Loopy belief propagation on the factor graph (the `-sp` path of
+// BN::marginals, model.cpp:313-317 -> BN::sum_product, model.cpp:736-753 ->
+// FactorGraph, graph.cpp:256-403).
+//
+// The reference's flooding schedule is Jacobi-style: all variable->factor
+// messages of an iteration read only the previous factor->variable messages,
+// all factor->variable messages read only the new variable->factor ones.  So
+// each phase is one parallel sweep over independent messages with a barrier
+// between phases.  BN message sets are tiny (KiB), the iteration count small
+// and data-dependent (stop on the largest relative change), so the whole loop
+// runs inside ONE workgroup: no launch per iteration, no host round trip for
+// the convergence test, messages stay in L1/L2.
+//
+// Arithmetic: fp64, as the reference.  Products run by ascending factor id
+// (variable side) and scope order (factor side); the reference walks
+// unordered_maps (graph.hh:50-51), so values agree up to rounding.
+#include <hip/hip_runtime.h>
+
+#include "bnpp_device.h"
+
+namespace bnpp {
+
+constexpr int kBpBlock = 1024;
+
+// largest value over the workgroup (every thread gets it); NaN never enters,
+// as in the reference (`if (err > maxerror)`, graph.cpp:353)
+__device__ double bp_block_max(double v, double *red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_xor(v, off, 64);
+        v = o > v ? o : v;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double m = red[0];
+    for (int w = 1; w < kBpBlock / 64; ++w) m = red[w] > m ? red[w] : m;
+    __syncthreads();               // red is rewritten by the next call
+    return m;
+}
+
+__global__ __launch_bounds__(kBpBlock) void sum_product_kernel(const BpArgs a) {
+    __shared__ double red[kBpBlock / 64];
+    const int tid = threadIdx.x;
+    // messages start uniform: 1 / |x| (graph.cpp:265-273)
+    for (int t = tid; t < a.n_msg; t += kBpBlock) {
+        const double u = 1.0 / a.cards[a.edge_var[a.item_edge[t]]];
+        a.v2f[t] = u;
+        a.f2v[t] = u;
+    }
+    __syncthreads();
+    int it = 0;
+    for (; it < a.max_iter; ++it) {
+        double lmax = 0.0;
+        // variable -> factor, one thread per edge (graph.cpp:335-362):
+        // Factor(x, 1.0) *= every other factor's message, normalize
+        for (int e = tid; e < a.n_edges; e += kBpBlock) {
+            const int v = a.edge_var[e], r = a.cards[v], o = a.msg_off[e];
+            const int b0 = a.v_edge_off[v], b1 = a.v_edge_off[v + 1];
+            double s = 0.0;
+            for (int x = 0; x < r; ++x) {
+                double p = 1.0;
+                for (int q = b0; q < b1; ++q) {
+                    const int e2 = a.v_edges[q];
+                    if (e2 != e) p = p * a.f2v[a.msg_off[e2] + x];
+                }
+                a.raw[o + x] = p;
+                s += p;
+            }
+            for (int x = 0; x < r; ++x) {
+                const double nw = a.raw[o + x] / s, old = a.v2f[o + x];
+                const double err = fabs(old - nw) / old;
+                if (err > lmax) lmax = err;
+                a.v2f[o + x] = nw;
+            }
+        }
+        __syncthreads();
+        // factor -> variable, one thread per message entry (graph.cpp:364-373):
+        // sum over the factor's entries with x_j fixed of F * the other
+        // variables' messages
+        for (int t = tid; t < a.n_msg; t += kBpBlock) {
+            const int e = a.item_edge[t], o = a.msg_off[e], x = t - o;
+            const int f = a.edge_fac[e], k0 = a.f_edge_off[f], k1 = a.f_edge_off[f + 1];
+            const uint32_t r = (uint32_t)a.cards[a.edge_var[e]], low = a.edge_stride[e];
+            const double *tab = a.tables + a.tab_off[f];
+            const uint32_t n = (uint32_t)((a.tab_off[f + 1] - a.tab_off[f]) / r);
+            double acc = 0.0;
+            for (uint32_t q = 0; q < n; ++q) {
+                const uint32_t i = (q / low) * (low * r) + (uint32_t)x * low + q % low;
+                double term = tab[i];
+                for (int k = k0; k < k1; ++k) {
+                    if (k == e) continue;
+                    const uint32_t d = (i / a.edge_stride[k]) % (uint32_t)a.cards[a.edge_var[k]];
+                    term = term * a.v2f[a.msg_off[k] + d];
+                }
+                acc += term;
+            }
+            a.raw[t] = acc;
+        }
+        __syncthreads();
+        // normalize (graph.cpp:374) and the relative change (graph.cpp:376-385)
+        for (int e = tid; e < a.n_edges; e += kBpBlock) {
+            const int o = a.msg_off[e], r = a.msg_off[e + 1] - o;
+            double s = 0.0;
+            for (int x = 0; x < r; ++x) s += a.raw[o + x];
+            for (int x = 0; x < r; ++x) {
+                const double nw = a.raw[o + x] / s, old = a.f2v[o + x];
+                const double err = fabs(old - nw) / old;
+                if (err > lmax) lmax = err;
+                a.f2v[o + x] = nw;
+            }
+        }
+        // (the barriers inside bp_block_max order these writes before the next reads)
+        if (bp_block_max(lmax, red) < a.eps) break;          // graph.cpp:328, uniform
+    }
+    __syncthreads();
+    // FactorGraph::marginal (graph.cpp:393-403): Factor(1.0) *= every message, normalize
+    for (int v = tid; v < a.n_vars; v += kBpBlock) {
+        const int r = a.cards[v], o = a.marg_off[v], b0 = a.v_edge_off[v], b1 = a.v_edge_off[v + 1];
+        double s = 0.0;
+        for (int x = 0; x < r; ++x) {
+            double p = 1.0;
+            for (int q = b0; q < b1; ++q) p = p * a.f2v[a.msg_off[a.v_edges[q]] + x];
+            a.marg[o + x] = p;
+            s += p;
+        }
+        for (int x = 0; x < r; ++x) a.marg[o + x] = a.marg[o + x] / s;
+    }
+    if (tid == 0) *a.iterations = it;
+}
+
+hipError_t launch_sum_product(const BpArgs &a, hipStream_t stream) {
+    hipLaunchKernelGGL(sum_product_kernel, dim3(1), dim3(kBpBlock), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace bnpp

@@ -939,4 +939,128 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
     BNPP_GUARD_END
 }
 
+// BN::marginals with options["sum-product"] (model.cpp:313-317): loopy BP on
+// the factor graph of the model's own factors (evidence is not used on this
+// path, as in the reference), FactorGraph::update(max_iter, eps) then one
+// marginal per variable (graph.cpp:256-403).  One workgroup runs the whole
+// loop (bp.hip).
+int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double eps, double *out, int *iterations,
+                     double *uptime_ms) {
+    BNPP_GUARD_BEGIN
+    if (!ctx || !m || !out) return set_err(BNPP_ERR_INVALID, "null argument");
+    if (max_iter < 0) return set_err(BNPP_ERR_INVALID, "max_iter must be >= 0");
+    const double t0 = now_ms();
+    const ModelData &d = m->d;
+    const int nv = (int)d.cards.size(), nf = (int)d.scopes.size();
+    // host image of every input array, laid out as on the device
+    std::vector<int32_t> f_edge_off(nf + 1, 0), edge_var, edge_fac, msg_off(1, 0), item_edge, v_edge_off(nv + 1, 0),
+        v_edges, marg_off(nv + 1, 0);
+    std::vector<uint32_t> edge_stride;
+    std::vector<int64_t> tab_off(nf + 1, 0);
+    for (int f = 0; f < nf; ++f) {
+        const std::vector<int> &sc = d.scopes[f];
+        int64_t size = 1;
+        for (int v : sc) size *= d.cards[v];
+        if (size >= ((int64_t)1 << 31)) return set_err(BNPP_ERR_UNSUPPORTED, "sum-product: factor table >= 2^31 entries");
+        int64_t st = size;
+        for (size_t j = 0; j < sc.size(); ++j) {
+            st /= d.cards[sc[j]];
+            const int e = (int)edge_var.size();
+            edge_var.push_back(sc[j]);
+            edge_fac.push_back(f);
+            edge_stride.push_back((uint32_t)st);
+            for (int x = 0; x < d.cards[sc[j]]; ++x) item_edge.push_back(e);
+            msg_off.push_back(msg_off.back() + d.cards[sc[j]]);
+            ++v_edge_off[sc[j] + 1];
+        }
+        f_edge_off[f + 1] = (int32_t)edge_var.size();
+        tab_off[f + 1] = tab_off[f] + size;
+    }
+    const int ne = (int)edge_var.size(), nmsg = msg_off.back();
+    for (int v = 0; v < nv; ++v) {
+        v_edge_off[v + 1] += v_edge_off[v];
+        marg_off[v + 1] = marg_off[v] + d.cards[v];
+    }
+    v_edges.resize(ne);
+    {
+        std::vector<int32_t> fill(v_edge_off.begin(), v_edge_off.end() - 1);
+        for (int e = 0; e < ne; ++e) v_edges[fill[edge_var[e]]++] = e;     // ascending edge = factor id
+    }
+    // one device block: inputs, then messages and outputs (256-B aligned pieces)
+    std::vector<unsigned char> host;
+    size_t off = 0;
+    auto place = [&](size_t bytes) {
+        const size_t o = off;
+        off = (off + bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    const size_t o_cards = place(4 * (size_t)nv), o_tabs = place(8 * (size_t)tab_off[nf]),
+                 o_tab_off = place(8 * (size_t)(nf + 1)), o_feo = place(4 * (size_t)(nf + 1)),
+                 o_ev = place(4 * (size_t)ne), o_ef = place(4 * (size_t)ne), o_es = place(4 * (size_t)ne),
+                 o_mo = place(4 * (size_t)(ne + 1)), o_ie = place(4 * (size_t)nmsg), o_veo = place(4 * (size_t)(nv + 1)),
+                 o_ve = place(4 * (size_t)ne), o_mgo = place(4 * (size_t)(nv + 1));
+    const size_t in_bytes = off;
+    const size_t o_v2f = place(8 * (size_t)nmsg), o_f2v = place(8 * (size_t)nmsg), o_raw = place(8 * (size_t)nmsg),
+                 o_marg = place(8 * (size_t)marg_off[nv]), o_it = place(4);
+    host.resize(in_bytes);
+    auto put = [&](size_t o, const void *src, size_t bytes) {
+        if (bytes) std::memcpy(host.data() + o, src, bytes);
+    };
+    std::vector<int32_t> cards32(d.cards.begin(), d.cards.end());
+    put(o_cards, cards32.data(), 4 * (size_t)nv);
+    for (int f = 0; f < nf; ++f) put(o_tabs + 8 * (size_t)tab_off[f], d.values[f].data(), 8 * d.values[f].size());
+    put(o_tab_off, tab_off.data(), 8 * tab_off.size());
+    put(o_feo, f_edge_off.data(), 4 * f_edge_off.size());
+    put(o_ev, edge_var.data(), 4 * (size_t)ne);
+    put(o_ef, edge_fac.data(), 4 * (size_t)ne);
+    put(o_es, edge_stride.data(), 4 * (size_t)ne);
+    put(o_mo, msg_off.data(), 4 * msg_off.size());
+    put(o_ie, item_edge.data(), 4 * (size_t)nmsg);
+    put(o_veo, v_edge_off.data(), 4 * v_edge_off.size());
+    put(o_ve, v_edges.data(), 4 * (size_t)ne);
+    put(o_mgo, marg_off.data(), 4 * marg_off.size());
+
+    hipStream_t s = ctx->c.stream;
+    unsigned char *dev = nullptr;
+    if (hipMalloc(&dev, off) != hipSuccess) return set_err(BNPP_ERR_OOM, "sum-product: device allocation");
+    struct Free {
+        unsigned char *p;
+        ~Free() { (void)hipFree(p); }
+    } guard{dev};
+    BpArgs a{};
+    a.n_vars = nv;
+    a.n_edges = ne;
+    a.n_msg = nmsg;
+    a.max_iter = max_iter;
+    a.eps = eps;
+    a.cards = reinterpret_cast<const int32_t *>(dev + o_cards);
+    a.tables = reinterpret_cast<const double *>(dev + o_tabs);
+    a.tab_off = reinterpret_cast<const int64_t *>(dev + o_tab_off);
+    a.f_edge_off = reinterpret_cast<const int32_t *>(dev + o_feo);
+    a.edge_var = reinterpret_cast<const int32_t *>(dev + o_ev);
+    a.edge_fac = reinterpret_cast<const int32_t *>(dev + o_ef);
+    a.edge_stride = reinterpret_cast<const uint32_t *>(dev + o_es);
+    a.msg_off = reinterpret_cast<const int32_t *>(dev + o_mo);
+    a.item_edge = reinterpret_cast<const int32_t *>(dev + o_ie);
+    a.v_edge_off = reinterpret_cast<const int32_t *>(dev + o_veo);
+    a.v_edges = reinterpret_cast<const int32_t *>(dev + o_ve);
+    a.marg_off = reinterpret_cast<const int32_t *>(dev + o_mgo);
+    a.v2f = reinterpret_cast<double *>(dev + o_v2f);
+    a.f2v = reinterpret_cast<double *>(dev + o_f2v);
+    a.raw = reinterpret_cast<double *>(dev + o_raw);
+    a.marg = reinterpret_cast<double *>(dev + o_marg);
+    a.iterations = reinterpret_cast<int32_t *>(dev + o_it);
+    int32_t it = 0;
+    hipError_t e = hipMemcpyAsync(dev, host.data(), in_bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = launch_sum_product(a, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, a.marg, 8 * (size_t)marg_off[nv], hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&it, a.iterations, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return set_err(BNPP_ERR_HIP, std::string("sum-product: ") + hipGetErrorString(e));
+    if (iterations) *iterations = it;
+    if (uptime_ms) *uptime_ms = now_ms() - t0;
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
 }  // extern "C"

@@ -24,6 +24,8 @@ struct SingleArgs {
     int64_t pool[kMaxPool];
 };
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream);
+// loopy BP, one workgroup (bp.hip)
+hipError_t launch_sum_product(const BpArgs &a, hipStream_t stream);
 
 enum DType { kF64 = 0, kF32 = 1 };
 

@@ -65,6 +65,7 @@ _SIGS = {
     "bnpp_ordering": (_I, [_P, _I, _IP, _IP, _I, _IP, _I, _IP, _IP]),
     "bnpp_partition": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _DP, _DP, _DP]),
     "bnpp_marginals": (_I, [_P, _P, _I, _IP, _IP, _I, _I, _IP, _I, _DP, _DP]),
+    "bnpp_sum_product": (_I, [_P, _P, _I, C.c_double, _DP, _IP, _DP]),
     "bnpp_marginals_tree": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, _DP, _DP]),
     "bnpp_marginals_tree_part": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, _I, _I, _DP, _IP, _DP]),
     "bnpp_plan_tree_part": (_I, [_P, _I, _IP, _IP, _I, _IP, _I, _I, _I, _I, _IP, _DP, _I]),
@@ -268,6 +269,21 @@ def marginals(ctx: Context, model: Model, evidence=None, heuristic: str = "mf", 
         res[t] = list(out[o:o + model.cards[t]])
         o += model.cards[t]
     return res, up.value
+
+
+def sum_product(ctx: Context, model: Model, max_iter: int = 10000, eps: float = 0.001):
+    """BN::marginals with options["sum-product"] (model.cpp:313-317): loopy BP
+    on the device (bnpp_sum_product) -> ({var: [p_0..p_k-1]}, iterations, uptime_ms).
+    Evidence is not used on this path, as in the reference."""
+    out = (C.c_double * max(sum(model.cards), 1))()
+    it, up = C.c_int(), C.c_double()
+    _check(_lib.bnpp_sum_product(ctx.handle, model.handle, max_iter, eps, out, C.byref(it), C.byref(up)),
+           "bnpp_sum_product")
+    res, o = {}, 0
+    for t in range(model.n_vars):
+        res[t] = list(out[o:o + model.cards[t]])
+        o += model.cards[t]
+    return res, it.value, up.value
 
 
 def marginals_tree(ctx: Context, model: Model, evidence=None, heuristic: str = "mf", dtype: int = F64,

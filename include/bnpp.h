@@ -174,6 +174,17 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
                              int heuristic, const int *order, int n_order, int n_targets, const int *targets,
                              int part, int n_parts, int dtype, double *out, int *owned, double *uptime_ms);
 
+/* BN::marginals with options["sum-product"] (model.cpp:313-317; the `bn -sp`
+ * flag): loopy BP on the factor graph of the model's factors,
+ * FactorGraph::update(max_iter, eps) (graph.cpp:298-332; the reference uses
+ * 10000, 0.001, model.cpp:749) then FactorGraph::marginal per variable
+ * (graph.cpp:393-403).  Evidence is not used, as in the reference.  fp64.
+ * out: sum(card) values, var-major; *iterations = update's return value
+ * (max_iter when it did not converge).  Factor tables >= 2^31 entries:
+ * BNPP_ERR_UNSUPPORTED. */
+int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double eps, double *out, int *iterations,
+                     double *uptime_ms);
+
 /* BN::variable_elimination (model.cpp:348-446) over the factors of `m` taken
  * as given (already conditioned by the caller): eliminates `vars` (heuristic
  * order, or exactly this order with BNPP_ORDER_GIVEN) and returns the result
