@@ -146,6 +146,12 @@ inline int64_t pack_dim_header(uint32_t card, uint32_t shift, bool pow2) {
 // occupies [msg_off[e], msg_off[e+1]) of v2f / f2v / raw; item_edge maps a
 // message entry back to its edge.  edge_stride[e]: stride of edge_var[e] in
 // the factor's table (row-major, last scope variable fastest).
+// lane class of a factor->variable sum by its number of terms: class 0 (< 16
+// terms) one lane, classes 1 / 2 / 3 (from 16 / 64 / 256 terms) 4 / 16 / 64 lanes
+__host__ __device__ constexpr int bp_lane_class(int64_t terms) {
+    return terms >= 256 ? 3 : terms >= 64 ? 2 : terms >= 16 ? 1 : 0;
+}
+constexpr int kBpLdsMsgMax = 4096;          // message entries kept in LDS (v2f + f2v: 64 KiB)
 struct BpArgs {
     int32_t n_vars, n_edges, n_msg, max_iter;
     double eps;
@@ -157,6 +163,11 @@ struct BpArgs {
     const uint32_t *edge_stride;            // n_edges
     const int32_t *msg_off;                 // n_edges + 1
     const int32_t *item_edge;               // n_msg
+    // factor->variable message entries grouped by lane class (bp_lane_class):
+    // class c holds cls_items[cls_off[c] .. cls_off[c+1])
+    int32_t cls_off[5];
+    const int32_t *cls_items;
+    int32_t msgs_in_lds;                    // v2f / f2v live in LDS (2 * n_msg doubles fit)
     const int32_t *v_edge_off, *v_edges;    // n_vars + 1, n_edges
     const int32_t *marg_off;                // n_vars + 1
     double *v2f, *f2v, *raw, *marg;

@@ -9,7 +9,11 @@
 // between phases.  BN message sets are tiny (KiB), the iteration count small
 // and data-dependent (stop on the largest relative change), so the whole loop
 // runs inside ONE workgroup: no launch per iteration, no host round trip for
-// the convergence test, messages stay in L1/L2.
+// the convergence test; the messages live in LDS when they fit (else L1/L2).
+// A factor->variable message entry is a sum over the factor's table with one
+// variable fixed: short sums take one lane, longer ones 4 / 16 / 64 lanes with
+// a butterfly reduction (large CPTs), so no lane walks a long serial chain of
+// dependent loads.
 //
 // Arithmetic: fp64, as the reference.  Products run by ascending factor id
 // (variable side) and scope order (factor side); the reference walks
@@ -38,14 +42,55 @@ __device__ double bp_block_max(double v, double *red) {
     return m;
 }
 
+// terms q0, q0 + step, ... of factor->variable message entry t
+__device__ __forceinline__ double bp_f2v_terms(const BpArgs &a, const double *v2f, int t, uint32_t q0,
+                                               uint32_t step) {
+    const int e = a.item_edge[t], o = a.msg_off[e], x = t - o;
+    const int f = a.edge_fac[e], k0 = a.f_edge_off[f], k1 = a.f_edge_off[f + 1];
+    const uint32_t r = (uint32_t)a.cards[a.edge_var[e]], low = a.edge_stride[e];
+    const double *tab = a.tables + a.tab_off[f];
+    const uint32_t n = (uint32_t)((a.tab_off[f + 1] - a.tab_off[f]) / r);
+    double acc = 0.0;
+    for (uint32_t q = q0; q < n; q += step) {
+        const uint32_t i = (q / low) * (low * r) + (uint32_t)x * low + q % low;
+        double term = tab[i];
+        for (int k = k0; k < k1; ++k) {
+            if (k == e) continue;
+            const uint32_t d = (i / a.edge_stride[k]) % (uint32_t)a.cards[a.edge_var[k]];
+            term = term * v2f[a.msg_off[k] + d];
+        }
+        acc += term;
+    }
+    return acc;
+}
+
+// the factor->variable sums of one lane class: G lanes per sum, butterfly
+// reduction (the same bits on every lane of the group)
+template <int G>
+__device__ __forceinline__ void bp_f2v_class(const BpArgs &a, const double *v2f, int c) {
+    const int grp = threadIdx.x / G, lane = threadIdx.x % G;
+    for (int q = a.cls_off[c] + grp; q < a.cls_off[c + 1]; q += kBpBlock / G) {
+        const int t = a.cls_items[q];
+        double acc = bp_f2v_terms(a, v2f, t, (uint32_t)lane, G);
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (lane == 0) a.raw[t] = acc;
+    }
+}
+
+// LDS: v2f and f2v live in LDS (2 * n_msg doubles of dynamic shared memory)
+template <bool LDS>
 __global__ __launch_bounds__(kBpBlock) void sum_product_kernel(const BpArgs a) {
     __shared__ double red[kBpBlock / 64];
+    extern __shared__ double lds_msgs[];
+    double *v2f = LDS ? lds_msgs : a.v2f;
+    double *f2v = LDS ? lds_msgs + a.n_msg : a.f2v;
     const int tid = threadIdx.x;
     // messages start uniform: 1 / |x| (graph.cpp:265-273)
     for (int t = tid; t < a.n_msg; t += kBpBlock) {
         const double u = 1.0 / a.cards[a.edge_var[a.item_edge[t]]];
-        a.v2f[t] = u;
-        a.f2v[t] = u;
+        v2f[t] = u;
+        f2v[t] = u;
     }
     __syncthreads();
     int it = 0;
@@ -61,41 +106,25 @@ __global__ __launch_bounds__(kBpBlock) void sum_product_kernel(const BpArgs a) {
                 double p = 1.0;
                 for (int q = b0; q < b1; ++q) {
                     const int e2 = a.v_edges[q];
-                    if (e2 != e) p = p * a.f2v[a.msg_off[e2] + x];
+                    if (e2 != e) p = p * f2v[a.msg_off[e2] + x];
                 }
                 a.raw[o + x] = p;
                 s += p;
             }
             for (int x = 0; x < r; ++x) {
-                const double nw = a.raw[o + x] / s, old = a.v2f[o + x];
+                const double nw = a.raw[o + x] / s, old = v2f[o + x];
                 const double err = fabs(old - nw) / old;
                 if (err > lmax) lmax = err;
-                a.v2f[o + x] = nw;
+                v2f[o + x] = nw;
             }
         }
         __syncthreads();
-        // factor -> variable, one thread per message entry (graph.cpp:364-373):
-        // sum over the factor's entries with x_j fixed of F * the other
-        // variables' messages
-        for (int t = tid; t < a.n_msg; t += kBpBlock) {
-            const int e = a.item_edge[t], o = a.msg_off[e], x = t - o;
-            const int f = a.edge_fac[e], k0 = a.f_edge_off[f], k1 = a.f_edge_off[f + 1];
-            const uint32_t r = (uint32_t)a.cards[a.edge_var[e]], low = a.edge_stride[e];
-            const double *tab = a.tables + a.tab_off[f];
-            const uint32_t n = (uint32_t)((a.tab_off[f + 1] - a.tab_off[f]) / r);
-            double acc = 0.0;
-            for (uint32_t q = 0; q < n; ++q) {
-                const uint32_t i = (q / low) * (low * r) + (uint32_t)x * low + q % low;
-                double term = tab[i];
-                for (int k = k0; k < k1; ++k) {
-                    if (k == e) continue;
-                    const uint32_t d = (i / a.edge_stride[k]) % (uint32_t)a.cards[a.edge_var[k]];
-                    term = term * a.v2f[a.msg_off[k] + d];
-                }
-                acc += term;
-            }
-            a.raw[t] = acc;
-        }
+        // factor -> variable (graph.cpp:364-373): sum over the factor's
+        // entries with x_j fixed of F * the other variables' messages
+        bp_f2v_class<1>(a, v2f, 0);
+        bp_f2v_class<4>(a, v2f, 1);
+        bp_f2v_class<16>(a, v2f, 2);
+        bp_f2v_class<64>(a, v2f, 3);
         __syncthreads();
         // normalize (graph.cpp:374) and the relative change (graph.cpp:376-385)
         for (int e = tid; e < a.n_edges; e += kBpBlock) {
@@ -103,10 +132,10 @@ __global__ __launch_bounds__(kBpBlock) void sum_product_kernel(const BpArgs a) {
             double s = 0.0;
             for (int x = 0; x < r; ++x) s += a.raw[o + x];
             for (int x = 0; x < r; ++x) {
-                const double nw = a.raw[o + x] / s, old = a.f2v[o + x];
+                const double nw = a.raw[o + x] / s, old = f2v[o + x];
                 const double err = fabs(old - nw) / old;
                 if (err > lmax) lmax = err;
-                a.f2v[o + x] = nw;
+                f2v[o + x] = nw;
             }
         }
         // (the barriers inside bp_block_max order these writes before the next reads)
@@ -119,7 +148,7 @@ __global__ __launch_bounds__(kBpBlock) void sum_product_kernel(const BpArgs a) {
         double s = 0.0;
         for (int x = 0; x < r; ++x) {
             double p = 1.0;
-            for (int q = b0; q < b1; ++q) p = p * a.f2v[a.msg_off[a.v_edges[q]] + x];
+            for (int q = b0; q < b1; ++q) p = p * f2v[a.msg_off[a.v_edges[q]] + x];
             a.marg[o + x] = p;
             s += p;
         }
@@ -129,7 +158,11 @@ __global__ __launch_bounds__(kBpBlock) void sum_product_kernel(const BpArgs a) {
 }
 
 hipError_t launch_sum_product(const BpArgs &a, hipStream_t stream) {
-    hipLaunchKernelGGL(sum_product_kernel, dim3(1), dim3(kBpBlock), 0, stream, a);
+    if (a.msgs_in_lds && a.n_msg <= kBpLdsMsgMax)
+        hipLaunchKernelGGL(sum_product_kernel<true>, dim3(1), dim3(kBpBlock), 2 * sizeof(double) * (size_t)a.n_msg,
+                           stream, a);
+    else
+        hipLaunchKernelGGL(sum_product_kernel<false>, dim3(1), dim3(kBpBlock), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -977,6 +977,16 @@ int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double ep
         tab_off[f + 1] = tab_off[f] + size;
     }
     const int ne = (int)edge_var.size(), nmsg = msg_off.back();
+    std::vector<int32_t> cls[4], cls_items;
+    for (int t = 0; t < nmsg; ++t) {
+        const int e = item_edge[t];
+        cls[bp_lane_class((tab_off[edge_fac[e] + 1] - tab_off[edge_fac[e]]) / d.cards[edge_var[e]])].push_back(t);
+    }
+    int32_t cls_off[5] = {0};
+    for (int c = 0; c < 4; ++c) {
+        cls_items.insert(cls_items.end(), cls[c].begin(), cls[c].end());
+        cls_off[c + 1] = (int32_t)cls_items.size();
+    }
     for (int v = 0; v < nv; ++v) {
         v_edge_off[v + 1] += v_edge_off[v];
         marg_off[v + 1] = marg_off[v] + d.cards[v];
@@ -998,7 +1008,8 @@ int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double ep
                  o_tab_off = place(8 * (size_t)(nf + 1)), o_feo = place(4 * (size_t)(nf + 1)),
                  o_ev = place(4 * (size_t)ne), o_ef = place(4 * (size_t)ne), o_es = place(4 * (size_t)ne),
                  o_mo = place(4 * (size_t)(ne + 1)), o_ie = place(4 * (size_t)nmsg), o_veo = place(4 * (size_t)(nv + 1)),
-                 o_ve = place(4 * (size_t)ne), o_mgo = place(4 * (size_t)(nv + 1));
+                 o_ve = place(4 * (size_t)ne), o_mgo = place(4 * (size_t)(nv + 1)),
+                 o_ci = place(4 * cls_items.size());
     const size_t in_bytes = off;
     const size_t o_v2f = place(8 * (size_t)nmsg), o_f2v = place(8 * (size_t)nmsg), o_raw = place(8 * (size_t)nmsg),
                  o_marg = place(8 * (size_t)marg_off[nv]), o_it = place(4);
@@ -1019,9 +1030,11 @@ int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double ep
     put(o_veo, v_edge_off.data(), 4 * v_edge_off.size());
     put(o_ve, v_edges.data(), 4 * (size_t)ne);
     put(o_mgo, marg_off.data(), 4 * marg_off.size());
+    put(o_ci, cls_items.data(), 4 * cls_items.size());
 
     hipStream_t s = ctx->c.stream;
     unsigned char *dev = nullptr;
+    if (hipSetDevice(ctx->c.device) != hipSuccess) return set_err(BNPP_ERR_HIP, "sum-product: hipSetDevice");
     if (hipMalloc(&dev, off) != hipSuccess) return set_err(BNPP_ERR_OOM, "sum-product: device allocation");
     struct Free {
         unsigned char *p;
@@ -1042,6 +1055,9 @@ int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double ep
     a.edge_stride = reinterpret_cast<const uint32_t *>(dev + o_es);
     a.msg_off = reinterpret_cast<const int32_t *>(dev + o_mo);
     a.item_edge = reinterpret_cast<const int32_t *>(dev + o_ie);
+    for (int c = 0; c < 5; ++c) a.cls_off[c] = cls_off[c];
+    a.cls_items = reinterpret_cast<const int32_t *>(dev + o_ci);
+    a.msgs_in_lds = nmsg <= kBpLdsMsgMax && !std::getenv("BNPP_BP_NO_LDS");
     a.v_edge_off = reinterpret_cast<const int32_t *>(dev + o_veo);
     a.v_edges = reinterpret_cast<const int32_t *>(dev + o_ve);
     a.marg_off = reinterpret_cast<const int32_t *>(dev + o_mgo);

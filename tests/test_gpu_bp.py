@@ -64,3 +64,18 @@ def test_sum_product_repeatable(ctx):
     r1 = bnpp.sum_product(ctx, m)
     r2 = bnpp.sum_product(ctx, m)
     assert r1[0] == r2[0] and r1[1] == r2[1]
+
+
+@pytest.mark.parametrize("model", ["pathfinder.uai", "ising10x10.uai"])
+def test_sum_product_global_messages_identical(ctx, model):
+    """Messages in global memory (BNPP_BP_NO_LDS, the path of models with more
+    than 4096 message entries) give the same bits as messages in LDS."""
+    import os
+    m = bnpp.Model.load(model_path(model))
+    lds = bnpp.sum_product(ctx, m, 10000, 1e-6)
+    os.environ["BNPP_BP_NO_LDS"] = "1"
+    try:
+        glb = bnpp.sum_product(ctx, m, 10000, 1e-6)
+    finally:
+        del os.environ["BNPP_BP_NO_LDS"]
+    assert lds[0] == glb[0] and lds[1] == glb[1]
