@@ -56,3 +56,16 @@ def test_cli_marginals_tree_equals_per_target():
         outs.append([l for l in out.splitlines() if "Executed" not in l])
     assert outs[0] == outs[1]
     assert any("Marginals" in l for l in outs[0])
+
+
+@pytest.mark.gpu
+def test_cli_sum_product_matches_reference(golden_sp):
+    """`bnpp model evid -mar -sp` (bn.cpp:177-178): loopy BP marginals, evidence
+    ignored as in the reference (model.cpp:313-317), printed like `bn`."""
+    case = next(c for c in golden_sp["cases"] if c["model"] == "asia.uai" and c["max_iter"] == 10000)
+    out = _cli(model_path("asia.uai"), model_path("asia.uai.evid"), "-mar", "-sp")
+    got = [float(m) for m in re.findall(r"^\d+ : ([-0-9.e+]+)\s*$", out, re.M)]
+    want = [p for v in sorted(case["marginals"], key=int) for p in case["marginals"][v]]
+    assert len(got) == len(want)
+    for a, b in zip(got, want):
+        assert abs(a - b) < 1e-6, (a, b)
