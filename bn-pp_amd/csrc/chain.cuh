@@ -213,9 +213,51 @@ constexpr int chain_v() {
            : FORM == kChainFwdV ? chain_fwd_v(ipow(K, F), (int)sizeof(T))
            : FORM == kChainSum ? 16 / (int)sizeof(T) : chain_bwd_v(ipow(K, F), (int)sizeof(T));
 }
-// per-wave LDS image of the forward forms: 64 rows of V * K^F entries (+16 B pad)
+// bytes of one forward output row, and of the part of it staged at a time
 template <typename T, int K, int F, int FORM>
-constexpr int chain_img_wave() { return 64 * (chain_v<T, K, F, FORM>() * ipow(K, F) * (int)sizeof(T) + kLdsRowPad); }
+constexpr int chain_row_bytes() { return chain_v<T, K, F, FORM>() * ipow(K, F) * (int)sizeof(T); }
+template <typename T, int K, int F, int FORM>
+constexpr int chain_part_bytes() { return chain_row_bytes<T, K, F, FORM>() < 128 ? chain_row_bytes<T, K, F, FORM>() : 128; }
+// per-wave LDS image of the forward forms: 64 row parts (+16 B pad)
+template <typename T, int K, int F, int FORM>
+constexpr int chain_img_wave() { return 64 * (chain_part_bytes<T, K, F, FORM>() + kLdsRowPad); }
+
+// Store one wave's rows of TS entries (row tid at out + tid * TS) through the
+// wave's LDS image, TH entries (<= 128 B) of every row at a time: each store
+// instruction then writes whole 128-B segments.  TS == TH is store_tiles.
+template <typename T, int TS, int TH>
+__device__ __forceinline__ void store_rows_parts(T *out, int64_t wave_tid0, int64_t n_tiles, const T (&row)[TS],
+                                                 unsigned char *lds) {
+    if constexpr (TS == TH) {
+        store_tiles<T, TS>(out, wave_tid0, n_tiles, row, lds);
+    } else {
+        static_assert(TS % TH == 0 && TH * (int)sizeof(T) % 16 == 0, "row parts of whole 16-B chunks");
+        const int lane = threadIdx.x & 63;
+        constexpr int rowp = TH * (int)sizeof(T) + kLdsRowPad;
+        constexpr int cpr = TH * (int)sizeof(T) / 16;
+        constexpr int EPC = 16 / (int)sizeof(T);
+        const int64_t valid = n_tiles - wave_tid0;
+        static_for<TS / TH>([&](auto pc) {
+            constexpr int p = decltype(pc)::value;
+            T part[TH];
+#pragma unroll
+            for (int i = 0; i < TH; ++i) part[i] = row[p * TH + i];
+            image_sync();
+            store_n<T, TH>(reinterpret_cast<T *>(lds + lane * rowp), part);
+            image_sync();
+#pragma unroll
+            for (int it = 0; it < cpr; ++it) {
+                const int q = it * 64 + lane;
+                const int src_lane = q / cpr, within = q % cpr;
+                if (src_lane < valid) {
+                    T x[EPC];
+                    load_n<T, EPC>(reinterpret_cast<const T *>(lds + src_lane * rowp + within * 16), x);
+                    store_n<T, EPC, kNtStore, true>(out + (wave_tid0 + src_lane) * TS + p * TH + within * EPC, x);
+                }
+            }
+        });
+    }
+}
 
 // waves per SIMD the register allocation must leave room for (0: compiler's
 // choice).  Measured on the 32x32 sweep: the forward 32-entry run at 3 waves
@@ -236,7 +278,7 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
     constexpr bool SUM = FORM == kChainSum;
     constexpr bool FWD = chain_fwd(FORM);
     constexpr int V = chain_v<T, K, F, FORM>();
-    static_assert(!FWD || V * N * (int)sizeof(T) <= 128, "forward rows go through the wave's LDS image");
+    static_assert(!FWD || V * N * (int)sizeof(T) <= 256, "forward rows go through the wave's LDS image");
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
     unsigned char *stage = dyn + kRedBytes;
@@ -371,8 +413,9 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
             for (int v = 0; v < V; ++v)
 #pragma unroll
                 for (int a = 0; a < N; ++a) row[v * N + a] = t[a][v];
-            store_tiles<T, V * N>(static_cast<T *>(c.out), tid0 + (threadIdx.x & ~63), c.n_tiles, row,
-                                  stage + (threadIdx.x >> 6) * chain_img_wave<T, K, F, FORM>());
+            store_rows_parts<T, V * N, chain_part_bytes<T, K, F, FORM>() / (int)sizeof(T)>(
+                static_cast<T *>(c.out), tid0 + (threadIdx.x & ~63), c.n_tiles, row,
+                stage + (threadIdx.x >> 6) * chain_img_wave<T, K, F, FORM>());
         }
     }
     if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
@@ -391,13 +434,13 @@ static hipError_t go_chain_level(const LevelArgs &a, int small_elems, int max_gr
 #define BNPP_CASE_CHAIN(T, K, F, FORM, DEP) \
     case 8192 + DEP * 2048 + FORM * 256 + K * 16 + F: return go_chain_level<T, K, F, FORM, DEP>(a, small_elems, max_grid, stream);
 #define BNPP_CASE_CHAIN_OK(T, K, F, FORM, DEP) case 8192 + DEP * 2048 + FORM * 256 + K * 16 + F: return true;
-// instantiated shapes: forward rows <= 128 B (V-wide forward for runs of
+// instantiated shapes: forward rows <= 256 B (V-wide forward for runs of
 // 4..16 entries), backward tables <= 64 entries
 // (V = 1 there); dep "any" only for tables <= 16 entries
 #define BNPP_CHAIN_ND(X, T, K, F, FORM) X(T, K, F, FORM, 0) X(T, K, F, FORM, 1)
 #define BNPP_CHAIN_F32(X, T) \
     BNPP_CHAIN_ND(X, T, 2, 2, 1) BNPP_CHAIN_ND(X, T, 2, 3, 1) BNPP_CHAIN_ND(X, T, 2, 4, 1) BNPP_CHAIN_ND(X, T, 2, 5, 1) \
-    BNPP_CHAIN_ND(X, T, 4, 2, 1) X(T, 2, 2, 1, 2) X(T, 2, 3, 1, 2) X(T, 2, 4, 1, 2) X(T, 4, 2, 1, 2) \
+    BNPP_CHAIN_ND(X, T, 2, 6, 1) BNPP_CHAIN_ND(X, T, 4, 2, 1) X(T, 2, 2, 1, 2) X(T, 2, 3, 1, 2) X(T, 2, 4, 1, 2) X(T, 4, 2, 1, 2) \
     BNPP_CHAIN_ND(X, T, 2, 2, 2) BNPP_CHAIN_ND(X, T, 2, 3, 2) BNPP_CHAIN_ND(X, T, 2, 4, 2) BNPP_CHAIN_ND(X, T, 2, 5, 2) \
     BNPP_CHAIN_ND(X, T, 2, 6, 2) BNPP_CHAIN_ND(X, T, 4, 2, 2) BNPP_CHAIN_ND(X, T, 4, 3, 2) \
     X(T, 2, 2, 2, 2) X(T, 2, 3, 2, 2) X(T, 2, 4, 2, 2) X(T, 4, 2, 2, 2) BNPP_CHAIN_SUM(X, T) \

@@ -201,7 +201,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         if (!ok) return fail("chain: summing run layout fits no kernel form");
         form = kChainSum;
     } else {
-        bool fwd = N * eb <= 128;
+        bool fwd = N * eb <= 256;                    // rows staged through LDS in 128-B parts
         for (int p = 0; fwd && p < F; ++p) {
             int64_t pl = 1;
             for (int q = p + 1; q < F; ++q) pl *= K;
