@@ -5,6 +5,7 @@ Run in the build container (needs /root/reference and `make -C oracle ref`):
 
     python tests/golden/make_golden.py          # everything
     python tests/golden/make_golden.py sp       # loopy BP fixtures only (sp_golden.json)
+    python tests/golden/make_golden.py corpus   # larger networks' PR (corpus_golden.json)
 
 It
   1. copies the reference's own model + fixture files that the tests use into
@@ -39,6 +40,9 @@ COPY = {
                   "insurance.uai", "win95pts.uai", "hailfinder.uai", "hepar2.uai", "andes.uai", "Water.uai",
                   "pathfinder.uai"],
 }
+# the reference's larger networks (corpus bench, tools/corpus_bench.py)
+CORPUS = ["Pigs.uai", "Link.uai", "Munin1.uai", "Munin2.uai", "Munin3.uai", "Munin4.uai", "Barley.uai",
+          "Mildew.uai", "Diabetes.uai"]
 
 
 def run(*args, timeout=900):
@@ -277,9 +281,67 @@ def sp_golden():
         json.dump({"cases": cases}, f)
 
 
+def ancestral_sample(m, rng):
+    """One joint sample of a BN (factor i = CPT of variable i, scope[0] = the
+    child, model.cpp:104-125): evidence drawn from it has P(e) > 0."""
+    cards, val = m["cards"], [-1] * len(m["cards"])
+    pending = set(range(len(cards)))
+    while pending:
+        done = []
+        for i in sorted(pending):
+            sc = m["scopes"][i]
+            if any(val[p] < 0 for p in sc[1:]):
+                continue
+            off, st = 0, 1
+            for p in reversed(sc[1:]):                    # row-major, last variable fastest
+                off += val[p] * st
+                st *= cards[p]
+            row = [m["values"][i][x * st + off] for x in range(cards[i])]
+            r, acc, pick = rng.random() * sum(row), 0.0, 0
+            for x, w in enumerate(row):
+                acc += w
+                if w > 0:
+                    pick = x
+                if w > 0 and r < acc:
+                    break
+            val[i] = pick
+            done.append(i)
+        assert done, "cyclic CPT structure"
+        pending.difference_update(done)
+    return val
+
+
+def corpus_golden():
+    """BN::partition (min-fill) on the reference's larger networks, without and
+    (three of them) with evidence sampled from the network; the reference's own
+    time is kept for the bench."""
+    rng = random.Random(99)
+    cases = []
+    for n in CORPUS:
+        shutil.copyfile(os.path.join(REF_MODELS, "bayesnets", n), model_path(n))
+        evs = ["-"]
+        if n in ("Pigs.uai", "Munin2.uai", "Diabetes.uai"):
+            m = synth.read_uai(model_path(n))
+            x = ancestral_sample(m, rng)
+            ev = {v: x[v] for v in range(len(m["cards"])) if rng.random() < 0.1}
+            synth.write_evidence(ev, model_path(n + ".evid"))
+            evs.append(n + ".evid")
+        for e in evs:
+            r = parse_kv(run("pr", model_path(n), model_path(e) if e != "-" else "-", "mf", timeout=1800))
+            w = int(run("width", model_path(n), "mf").split()[1])
+            cases.append({"model": n, "evidence": e, "heuristic": "mf", "Z": r["Z"], "log10Z": r["log10Z"],
+                          "ref_uptime_ms": r["uptime_ms"], "ref_width": w})
+            print("corpus", n, e, r["log10Z"], r["uptime_ms"], w)
+    with open(os.path.join(HERE, "corpus_golden.json"), "w") as f:
+        json.dump({"cases": cases}, f, indent=1)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["sp"]:
         sp_golden()
+    elif sys.argv[1:] == ["corpus"]:
+        corpus_golden()
     else:
         main()
         sp_golden()
+        corpus_golden()

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""The reference's larger networks (Pigs, Link, Munin1-4, Barley, Mildew,
+Diabetes; tests/golden/corpus_golden.json): PR (min-fill, fp64) on the device
+against BN::partition timed on this box's CPU (oracle/_ref/ref_harness, one
+core; cases the golden run found slower than --ref-cap seconds keep the build
+container's time), plus all marginals from one bucket tree (fp64), for which
+the reference would run one VE per variable (model.cpp:326-334: ~n_vars x PR).
+
+    python tools/corpus_bench.py > gpurun_out/corpus_bench.jsonl
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+REPO = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(REPO, "bn-pp_amd", "python"))
+import bnpp  # noqa: E402
+
+MODELS = os.path.join(REPO, "tests", "golden", "models")
+HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+
+
+def ref_pr_ms(model, ev):
+    out = subprocess.run([HARNESS, "pr", os.path.join(MODELS, model), os.path.join(MODELS, ev) if ev != "-" else "-",
+                          "mf"], capture_output=True, text=True, timeout=300, check=True).stdout
+    kv = dict(line.split()[:2] for line in out.splitlines() if len(line.split()) == 2)
+    return float(kv["uptime_ms"])
+
+
+def timed(fn, reps=3):
+    fn()                                                     # warm-up (planning caches, module load)
+    ts = []
+    for _ in range(reps):
+        r = fn()
+        ts.append(r[-1])
+    return r, statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref-cap", type=float, default=60.0, help="seconds: slower reference runs are not re-timed")
+    args = ap.parse_args()
+    with open(os.path.join(REPO, "tests", "golden", "corpus_golden.json")) as f:
+        cases = json.load(f)["cases"]
+    ctx = bnpp.Context(0)
+    for c in cases:
+        m = bnpp.Model.load(os.path.join(MODELS, c["model"]))
+        ev = bnpp.load_evidence(os.path.join(MODELS, c["evidence"])) if c["evidence"] != "-" else {}
+        (lz, _, _), pr_ms = timed(lambda: bnpp.partition(ctx, m, ev, "mf", bnpp.F64))
+        rec = {"instance": c["model"], "evidence": c["evidence"], "task": "PR", "dtype": "f64", "log10Z": lz,
+               "ref_log10Z": c["log10Z"], "abs_err_log10Z": abs(lz - c["log10Z"]), "gpu_uptime_ms": pr_ms,
+               "ref_width": c["ref_width"]}
+        if c["ref_uptime_ms"] <= args.ref_cap * 1e3 and os.path.exists(HARNESS):
+            rec["ref_ms"], rec["ref_where"] = ref_pr_ms(c["model"], c["evidence"]), "this box"
+        else:
+            rec["ref_ms"], rec["ref_where"] = c["ref_uptime_ms"], "build container (golden run)"
+        rec["speedup"] = rec["ref_ms"] / pr_ms
+        print(json.dumps(rec), flush=True)
+        (marg, _), mar_ms = timed(lambda: bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F64))
+        worst = max(abs(sum(p) - 1.0) for p in marg.values() if p)
+        rec2 = {"instance": c["model"], "evidence": c["evidence"], "task": "MAR (bucket tree)", "dtype": "f64",
+                "gpu_uptime_ms": mar_ms, "n_vars": m.n_vars, "max_sum_err": worst,
+                "ref_estimate_ms": rec["ref_ms"] * (m.n_vars - len(ev)),
+                "ref_note": "reference MAR = one VE per non-evidence variable (model.cpp:326-334) ~ n x PR; not run"}
+        rec2["speedup_vs_estimate"] = rec2["ref_estimate_ms"] / mar_ms
+        print(json.dumps(rec2), flush=True)
+
+
+if __name__ == "__main__":
+    main()
