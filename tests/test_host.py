@@ -231,3 +231,47 @@ def test_plan_uses_summing_runs():
     finally:
         del os.environ["BNPP_NO_CHAIN"]
     assert fused[6] < 0.6 * plain[6]
+
+
+def _chain_forms(capfd, m, order, env, kind=0):
+    """kernel forms the planner picks (BNPP_DEBUG_CHAIN lines on fd 2)."""
+    old = {k: os.environ.get(k) for k in list(env) + ["BNPP_DEBUG_CHAIN"]}
+    os.environ.update(env, BNPP_DEBUG_CHAIN="1")
+    try:
+        capfd.readouterr()
+        bnpp.plan_stats(m, kind, {}, "mf", dtype=bnpp.F32, order=order)
+        err = capfd.readouterr().err
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    forms = set()
+    for line in err.splitlines():
+        if line.startswith("[chain] run form"):
+            p = line.split()
+            forms.add((int(p[3]), int(p[5].split("=")[1])))      # (form, F)
+    return forms
+
+
+def test_plan_short_forward_runs_use_vector_form(capfd):
+    """Forward runs capped at 3 buckets on a tall sweep take kChainFwdV (form 4)
+    unless BNPP_NO_CHAIN_FWDV; the same runs then use the one-entry form 1."""
+    from bnpp import synth
+    m = bnpp.Model.from_dict(synth.ising_grid(16, 5, seed=11))
+    col = [i * 5 + j for j in range(5) for i in range(16)]
+    forms = _chain_forms(capfd, m, col, {"BNPP_CHAIN_RUN_MAX": "3"})
+    assert (4, 3) in forms and (1, 3) not in forms, forms
+    forms = _chain_forms(capfd, m, col, {"BNPP_CHAIN_RUN_MAX": "3", "BNPP_NO_CHAIN_FWDV": "1"})
+    assert (1, 3) in forms and (4, 3) not in forms, forms
+
+
+def test_plan_forward_runs_of_six(capfd):
+    """Binary fp32 sweeps of a checkpointed bucket tree fuse 6 forward buckets
+    per pass (256-B rows staged in 128-B parts) and 6 backward ones."""
+    from bnpp import synth
+    m = bnpp.Model.from_dict(synth.ising_grid(16, 5, seed=11))
+    col = [i * 5 + j for j in range(5) for i in range(16)]
+    forms = _chain_forms(capfd, m, col, {"BNPP_TREE_SLOTS": "3"}, kind=3)
+    assert (1, 6) in forms and (2, 6) in forms, forms
