@@ -265,7 +265,11 @@ __device__ __forceinline__ void store_rows_parts(T *out, int64_t wave_tid0, int6
 // best left alone.
 template <typename T, int K, int F, int FORM>
 constexpr int chain_min_waves() {
+#ifdef BNPP_CHAIN_MW_WIDE
+    return FORM == kChainFwd && sizeof(T) == 4 && ipow(K, F) >= 32 ? 3 : 1;
+#else
     return FORM == kChainFwd && sizeof(T) == 4 && ipow(K, F) == 32 ? 3 : 1;
+#endif
 }
 
 template <typename T, int K, int F, int FORM, int DEP>
