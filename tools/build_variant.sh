@@ -13,5 +13,5 @@ for f in launch k_generic_f32 k_generic_f64 k_stream_f32 k_stream_f64 k_chain_f3
 done
 wait
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib_$name/libbnpp.so build_$name/*.o \
-    build/plan.o build/order.o build/model_io.o build/runtime.o build/capi.o build/bn_api.o -Wl,-soname,libbnpp.so -pthread
+    build/bp.o build/plan.o build/order.o build/model_io.o build/runtime.o build/capi.o build/bn_api.o -Wl,-soname,libbnpp.so -pthread
 echo "built lib_$name"
