@@ -262,8 +262,9 @@ __device__ __forceinline__ void store_rows_parts(T *out, int64_t wave_tid0, int6
 // waves per SIMD the register allocation must leave room for (0: compiler's
 // choice).  Measured on the 32x32 sweep: the forward 32-entry run at 3 waves
 // 7.26 -> 6.57 ms per 2^32 message (4 waves spills); the same bound on the
-// 64-entry runs takes the 32x32 PR 1.23 -> 1.19 s; the backward runs are best
-// left alone.
+// 64-entry runs takes the 32x32 PR 1.23 -> 1.19 s and MAR 3.95 -> 3.81 s (2
+// waves: 3.92 s, 4 waves spills: 5.03 s); the backward runs are best left to
+// the compiler (bounds of 2 or 3 waves: same or slower, tools/ab_mar.sh).
 template <typename T, int K, int F, int FORM>
 constexpr int chain_min_waves() {
     return FORM == kChainFwd && sizeof(T) == 4 && ipow(K, F) >= 32 ? 3 : 1;

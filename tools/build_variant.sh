@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../bn-pp_amd"
 name=$1; flags=$2
-make -s lib/libbnpp.so
+make -s -j8 lib/libbnpp.so
 mkdir -p build_$name lib_$name
 for f in launch k_generic_f32 k_generic_f64 k_stream_f32 k_stream_f64 k_chain_f32 k_chain_f64; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Icsrc -I../include $flags \
