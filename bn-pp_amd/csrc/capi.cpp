@@ -8,12 +8,14 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "model_io.hpp"
@@ -141,6 +143,44 @@ std::vector<View> source_views(const ModelData &d, const std::vector<int> &ev) {
     return views;
 }
 
+// Checkpoint-slot counts chosen by the bucket-tree search below, keyed on
+// everything the plan's arena size depends on except the budget.  The search evaluates ~6 chain
+// plans (≈60 ms on the 32x32 grid); a repeated MAR call on the same model then
+// builds one plan.
+// An entry holds for every budget in [need_ok, need_fail): the arena need of
+// the chosen count and of the smallest count found not to fit.
+struct SlotMemo {
+    struct Entry {
+        uint64_t key;
+        int slots;
+        int64_t need_ok, need_fail;
+    };
+    std::mutex mu;
+    std::vector<Entry> entries;
+};
+SlotMemo &slot_memo() {
+    static SlotMemo m;
+    return m;
+}
+uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<int>> &scopes, const std::vector<int> &ord,
+                  const std::vector<int> &targets, int eb, int part, int n_parts) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+    auto mixv = [&](const std::vector<int> &v) {
+        mix(v.size());
+        for (int x : v) mix((uint32_t)x);
+    };
+    mixv(cards);
+    mix(scopes.size());
+    for (const auto &sc : scopes) mixv(sc);
+    mixv(ord);
+    mixv(targets);
+    mix((uint64_t)eb);
+    mix((uint64_t)part);
+    mix((uint64_t)n_parts);
+    return h;
+}
+
 // Build the VE plans for a job: kind 0 = partition, kind 1 = marginals of targets.
 int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
                 int n_order, const std::vector<int> &targets, std::vector<VEPlan> &plans, int &max_width,
@@ -212,19 +252,49 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             std::string msg;
             VEPlan best;
             int lo = 1, hi = 64, best_s = 0;
+            const uint64_t key = slot_key(d.cards, scopes, ord, targets, chain_eb, part, n_parts);
+            int memo_s = 0;
+            {
+                std::lock_guard<std::mutex> g(slot_memo().mu);
+                for (const SlotMemo::Entry &e : slot_memo().entries)
+                    if (e.key == key && e.need_ok <= budget && budget < e.need_fail) memo_s = e.slots;
+            }
+            if (memo_s > 0) {                             // the search would land on the same count
+                VEPlan cp;
+                if (plan_bucket_tree_chain(d.cards, views, ord, targets, memo_s, part, n_parts, cp, &msg, chain_eb) &&
+                    need(cp) <= budget) {
+                    best_s = memo_s;
+                    best = std::move(cp);
+                    lo = hi + 1;
+                }
+            }
+            int64_t need_ok = 0, need_fail = INT64_MAX;
+            bool exact = true;                            // every probe planned: the bracket is valid
             while (lo <= hi) {
                 int mid = (lo + hi) / 2;
                 VEPlan cp;
-                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, part, n_parts, cp, &msg, chain_eb)) break;
-                if (need(cp) <= budget) {
+                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, part, n_parts, cp, &msg, chain_eb)) {
+                    exact = false;
+                    break;
+                }
+                const int64_t nb = need(cp);
+                if (nb <= budget) {
                     best_s = mid;
                     best = std::move(cp);
+                    need_ok = nb;
                     lo = mid + 1;
                 } else {
+                    need_fail = std::min(need_fail, nb);
                     hi = mid - 1;
                 }
             }
             if (best_s > 0) {
+                if (best_s != memo_s && exact) {
+                    std::lock_guard<std::mutex> g(slot_memo().mu);
+                    auto &en = slot_memo().entries;
+                    if (en.size() >= 64) en.erase(en.begin());
+                    en.push_back({key, best_s, need_ok, need_fail});
+                }
                 if (std::getenv("BNPP_TIMING")) std::fprintf(stderr, "[bnpp] bucket tree: %d checkpoint slots\n", best_s);
                 plans.back() = std::move(best);
             }

@@ -275,3 +275,36 @@ def test_plan_forward_runs_of_six(capfd):
     col = [i * 5 + j for j in range(5) for i in range(16)]
     forms = _chain_forms(capfd, m, col, {"BNPP_TREE_SLOTS": "3"}, kind=3)
     assert (1, 6) in forms and (2, 6) in forms, forms
+
+
+def test_checkpoint_slot_memo_matches_fresh_search():
+    """The bucket-tree planner remembers its checkpoint-slot search per model
+    and budget bracket (capi.cpp SlotMemo): repeated and interleaved budgets in
+    one process give the plans a fresh process's search gives."""
+    import json
+    import subprocess
+    import sys
+    m = bnpp.Model.load(model_path("ising10x10.uai"))
+    col = [r * 10 + c for c in range(10) for r in range(10)]
+    full_arena = bnpp.plan_stats(m, 3, {}, "mf", order=col)[1]
+    budgets = [full_arena * f / 1e9 for f in (0.5, 0.75, 0.5, 0.95, 0.6, 0.52)]
+
+    def stats(b):
+        os.environ["BNPP_MEM_BUDGET_GB"] = repr(b)
+        try:
+            return list(bnpp.plan_stats(m, 3, {}, "mf", order=col))
+        finally:
+            del os.environ["BNPP_MEM_BUDGET_GB"]
+
+    here = [stats(b) for b in budgets]
+    code = ("import os, sys, json, bnpp\n"
+            "m = bnpp.Model.load(sys.argv[1])\n"
+            "col = [r * 10 + c for c in range(10) for r in range(10)]\n"
+            "os.environ['BNPP_MEM_BUDGET_GB'] = sys.argv[2]\n"
+            "print(json.dumps(list(bnpp.plan_stats(m, 3, {}, 'mf', order=col))))\n")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join(sys.path))
+    for b, got in zip(budgets, here):
+        out = subprocess.run([sys.executable, "-c", code, model_path("ising10x10.uai"), repr(b)], env=env,
+                             capture_output=True, text=True, timeout=120, check=True).stdout
+        assert json.loads(out.strip().splitlines()[-1]) == got
+    assert here[0] == here[2] and here[0] != here[1] and here[1][1] <= budgets[1] * 1e9

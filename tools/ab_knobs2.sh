@@ -1,5 +1,4 @@
 #!/bin/bash
-# 32x32 bucket-tree MAR under planner knobs (env), 3 calls each on one context.
 set -o pipefail
 mkdir -p gpurun_out
 run() {
@@ -8,8 +7,9 @@ run() {
   python -c "
 import json; d=[json.loads(x) for x in open('gpurun_out/abk_$tag.jsonl') if '\"mar\"' in x]; print('$tag', [round(x['uptime_ms'],1) for x in d], d[-1]['p_mid'])"
 }
-run base BNPP_NONE=1
-run run5 BNPP_CHAIN_RUN_MAX=5
-run slots36 BNPP_TREE_SLOTS=36
-run slots40 BNPP_TREE_SLOTS=40
-run base2 BNPP_NONE=1
+run base BNPP_TIMING=1
+run s40 BNPP_TREE_SLOTS=40 BNPP_TIMING=1
+run s38 BNPP_TREE_SLOTS=38
+run s34 BNPP_TREE_SLOTS=34
+run s41 BNPP_TREE_SLOTS=41
+run s40b BNPP_TREE_SLOTS=40
