@@ -80,7 +80,8 @@ struct LevelArgs {
 
 // loads of the big input of a stream bucket, relative to one thread's tile
 enum BigClass : int32_t { kBigRow = 1, kBigCol = 2, kBigFull = 3, kBigDirect = 4, kBigOne = 5,
-                                kBigInter2 = 6, kBigInter4 = 7 };   // summed var fastest in the big input, card 2 / 4
+                                kBigInter2 = 6, kBigInter4 = 7,    // summed var fastest in the big input, card 2 / 4
+                                kBigSlab = 8 };   // slab form (slab.cuh): v1 = card of output dim 0, v2 = s per lane
 constexpr int kStreamSmallMax = 4096;      // entries: inputs at most this big go to LDS
 constexpr int kStreamLdsBudget = 32768;    // bytes of LDS for the small inputs
 
@@ -92,6 +93,8 @@ __host__ __device__ inline int nin_class(int n_in) { return n_in <= 1 ? 1 : n_in
 __host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return nin_class(n_in) * 64 + v1 * 8 + v2; }
 // stream kernels: 4096 + big-class * 256 + v1 * 16 + v2  (v1, v2 <= 8)
 __host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 256 + v1 * 16 + v2; }
+// slab kernels (slab.cuh): K summed values, C0 entries of output dim 0, V slow-dim entries per lane
+__host__ __device__ constexpr int slab_key(int k, int c0, int v) { return 16384 + k * 256 + c0 * 16 + v; }
 
 // Chain (sweep) form: F consecutive buckets of an elimination chain in one
 // pass.  Input 0 is the message entering the run; bucket j of the run sums

@@ -163,7 +163,7 @@ SlotMemo &slot_memo() {
     return m;
 }
 uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<int>> &scopes, const std::vector<int> &ord,
-                  const std::vector<int> &targets, int eb, int part, int n_parts) {
+                  const std::vector<int> &targets, int eb, int chain_eb, int part, int n_parts) {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
     auto mixv = [&](const std::vector<int> &v) {
@@ -175,7 +175,8 @@ uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<i
     for (const auto &sc : scopes) mixv(sc);
     mixv(ord);
     mixv(targets);
-    mix((uint64_t)eb);
+    mix((uint64_t)eb);                    // the dtype: arena bytes scale with it
+    mix((uint64_t)chain_eb);              // fused runs on/off change the plan
     mix((uint64_t)part);
     mix((uint64_t)n_parts);
     return h;
@@ -252,7 +253,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             std::string msg;
             VEPlan best;
             int lo = 1, hi = 64, best_s = 0;
-            const uint64_t key = slot_key(d.cards, scopes, ord, targets, chain_eb, part, n_parts);
+            const uint64_t key = slot_key(d.cards, scopes, ord, targets, eb, chain_eb, part, n_parts);
             int memo_s = 0;
             {
                 std::lock_guard<std::mutex> g(slot_memo().mu);
@@ -281,7 +282,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                 if (nb <= budget) {
                     best_s = mid;
                     best = std::move(cp);
-                    need_ok = nb;
+                    need_ok = std::max(need_ok, nb);      // valid for budgets >= every fitting probe's need
                     lo = mid + 1;
                 } else {
                     need_fail = std::min(need_fail, nb);
@@ -525,8 +526,9 @@ int bnpp_ctx_create(int device, bnpp_ctx **out) {
     std::unique_ptr<bnpp_ctx> ctx(new bnpp_ctx);
     ctx->c.device = device;
     int per_cu = 3;          // measured: 3 workgroups per CU beat 4 and 8 on the bench bucket and the 32x32 sweep
-    if (const char *g = std::getenv("BNPP_GRID_PER_CU")) per_cu = std::max(1, std::min(64, std::atoi(g)));
-    ctx->c.max_grid = prop.multiProcessorCount * per_cu;
+    if (const char *g = std::getenv("BNPP_GRID_PER_CU")) per_cu = std::max(0, std::min(64, std::atoi(g)));
+    // 0: flat grid, one virtual block per workgroup (no grid-stride)
+    ctx->c.max_grid = per_cu == 0 ? INT32_MAX : prop.multiProcessorCount * per_cu;
     if ((e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking)) != hipSuccess)
         return set_err(BNPP_ERR_HIP, hipGetErrorString(e));
     *out = ctx.release();

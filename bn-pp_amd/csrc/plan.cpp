@@ -467,6 +467,39 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         if (!b.divide && n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 && !(off && *off == '1')) {
             int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
             int64_t s1 = merged.size() < 2 ? 0 : merged[1].s[big];
+            // slab form (slab.cuh): the big input is k slabs contiguous along the
+            // output's slow dim (its only other dim, of card 1/2/4, it does not
+            // vary along), every small input is constant along that slow dim
+            int slab_v = 0, slab_c0 = 1;
+            {
+                const char *ns = std::getenv("BNPP_NO_SLAB");
+                const bool two = merged.size() == 2;
+                const Dim *sd = two ? &merged[1] : merged.size() == 1 ? &merged[0] : nullptr;
+                slab_c0 = two ? (int)merged[0].card : 1;
+                bool ok = !(ns && *ns == '1') && sd && k >= 1 && k <= 4 && sd->s[big] == 1 &&
+                          (!two || merged[0].s[big] == 0) && (slab_c0 == 1 || slab_c0 == 2 || slab_c0 == 4);
+                for (int i = 0; ok && i < n; ++i)
+                    if (i != big && sd->s[i] != 0) ok = false;
+                if (ok) {
+                    int vn = eb == 4 ? (slab_c0 == 1 ? 4 : slab_c0 == 2 ? 2 : 1) : (slab_c0 == 1 ? 2 : 1);
+                    if ((int64_t)sd->card % vn || b.in[big].base % vn || es[big] % vn) vn = 1;
+                    slab_v = vn;
+                }
+            }
+            if (slab_v > 0) {
+                v1 = slab_c0;
+                v2 = slab_v;
+                d.v1 = v1;
+                d.v2 = v2;
+                d.n_tiles = out_size / (v1 * v2);
+                d.big = big;
+                d.bcls = kBigSlab;
+                for (int i = 0; i < n; ++i) {
+                    d.in_span[i] = (int32_t)std::min<int64_t>(span[i], INT32_MAX);
+                    d.in_lds_off[i] = 0;
+                }
+                d.small_elems = 0;
+            } else {
             // optional narrow tile: when the big input is constant along the
             // fastest output dim and v1 entries already fill a 16-B store, drop
             // v2 (one scalar big load per summed value, stores coalesced as is)
@@ -559,6 +592,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 if (i != big) o += (int32_t)((span[i] + 3) & ~3);       // keep 16-B alignment
             }
             d.small_elems = o;
+            }
         }
     }
     if (b.divide) {
@@ -1544,6 +1578,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
         it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf)
+                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2)
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2) : variant_key(it.d.n_in, it.d.v1, it.d.v2);
     });
     for (const Item &it : items)

@@ -218,6 +218,72 @@ def test_interleaved_broadcast_rows(ctx, k, kq, n_other):
     assert max(abs(a - b) / abs(b) for a, b in zip(vals, want)) < 1e-6
 
 
+@pytest.mark.parametrize("k,c0,scards", [(4, 4, [4] * 6), (2, 2, [2] * 13), (2, 4, [2] * 12), (3, 1, [3] * 8),
+                                         (1, 2, [2] * 13), (2, 2, [3] * 8), (4, 1, [2] * 12), (3, 4, [3, 2] * 4)])
+def test_slab_form_buckets(ctx, k, c0, scards):
+    """Slab form (slab.cuh, flat grid): the big input holds the summed variable
+    x as its slowest dim (k slabs contiguous along the output's slow index S),
+    small inputs depend on (x, y) only, the output is (S..., y).  Every chain
+    position of the big input; odd S cards force the one-entry-per-lane tile.
+    fp64 bit-exact against the oracle, fp32 1e-6 relative."""
+    rng = random.Random(k * 1000 + c0 * 100 + len(scards))
+    x, y = 0, 1
+    S = list(range(2, 2 + len(scards)))
+    cards = {x: k, y: c0}
+    for v, c in zip(S, scards):
+        cards[v] = c
+    size = k
+    for c in scards:
+        size *= c
+    big = ([x] + S, [rng.uniform(0.5, 2.0) for _ in range(size)])
+    ys = [y] if c0 > 1 else []
+    pair = ([x] + ys, [rng.uniform(0.5, 2.0) for _ in range(k * c0)])
+    unary = ([x], [rng.uniform(0.5, 2.0) for _ in range(k)])
+    side = (ys, [rng.uniform(0.5, 2.0) for _ in range(c0)])
+    elim = x if k > 1 else -1
+    for ins in ([big, pair], [pair, big], [unary, big, pair], [unary, pair, big, side], [big, side, unary]):
+        fs = [refcpu.Factor.new(sc, cards, v) for sc, v in ins]
+        if elim >= 0:
+            ref = refcpu.bucket(fs, elim, k)
+        else:
+            ref = fs[0]
+            for f in fs[1:]:
+                ref = ref.product(f)
+        planned = S + ys + ([x] if elim < 0 else [])
+        t = torch.tensor(ref.values, dtype=torch.float64).reshape([cards[v] for v in ref.scope])
+        want = t.permute([ref.scope.index(v) for v in planned]).reshape(-1).tolist()
+        scope, vals = run_bucket(ctx, bnpp.F64, cards, ins, elim, out_vars=planned)
+        assert vals == want, [s for s, _ in ins]
+        scope, vals = run_bucket(ctx, bnpp.F32, cards, ins, elim, out_vars=planned)
+        assert max(abs(a - b) / abs(b) for a, b in zip(vals, want)) < 1e-6
+
+
+def test_slab_level_kernels_in_ve(ctx, monkeypatch, capfd):
+    """Whole VE runs with fused sweep runs off: a 12x12 min-fill plan and a
+    14x14 column sweep hold slab-form buckets (bcls 8 in the plan dump), run by
+    the slab level kernel (flat grid, rescaling, max tracking).  fp64 log10 Z
+    identical with the slab form off, and the oracle's within 1e-13."""
+    from bnpp import synth
+    monkeypatch.setenv("BNPP_NO_CHAIN", "1")
+    for n, order in ((12, None), (14, [r * 14 + c for c in range(14) for r in range(14)])):
+        d = synth.ising_grid(n, n, seed=3)
+        m = bnpp.Model.from_dict(d)
+        monkeypatch.setenv("BNPP_DUMP_PLAN", "1")
+        capfd.readouterr()
+        lz_slab = bnpp.partition(ctx, m, {}, "mf", bnpp.F64, order=order)[0]
+        assert "bcls=8" in capfd.readouterr().err
+        monkeypatch.delenv("BNPP_DUMP_PLAN")
+        monkeypatch.setenv("BNPP_NO_SLAB", "1")
+        lz_gen = bnpp.partition(ctx, m, {}, "mf", bnpp.F64, order=order)[0]
+        monkeypatch.delenv("BNPP_NO_SLAB")
+        assert lz_slab == lz_gen
+        if order is None:
+            rz = refcpu.Model.from_dict(d).partition({}, "mf")[0]
+            assert abs(math.log10(rz) - lz_slab) < 1e-13
+        f32 = bnpp.partition(ctx, m, {}, "mf", bnpp.F32, order=order)[0]
+        assert abs(f32 - lz_slab) < 1e-6 * abs(lz_slab)
+
+
 def test_permuted_output_layout(ctx):
     """Any permutation of the output scope is accepted and gives the same table, transposed."""
     rng = random.Random(5)
