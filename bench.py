@@ -4,9 +4,12 @@
 Workload (BASELINE config 5 restated): one VE bucket of a
 4-state Potts model,  msg(S_1..S_w, y) = sum_x m(x, S_1..S_w) * f(x, y),  all
 cards k = 4, w = 14, fp32  =>  4^16 = 4.29e9 factor-entries per step, inputs
-resident in HBM.  With --gpus N each rank evaluates its own block of a global
-bucket whose output is split on a leading variable (weak scaling: fixed work
-per GPU, no data-path collective; one barrier + max-reduce of the timer).
+resident in HBM.  With --gpus N every rank evaluates its own independent bucket
+of that shape (its own seed): weak scaling, fixed work per GPU, no data-path
+collective, one barrier + max-reduce of the timer.  Checks: the checksum of
+checksums (sum of the output = sum_x rowsum(m)_x * rowsum(f)_x) and an exact
+spot check of 512 random output entries against the same arithmetic in torch
+(fp32 products, sums in the reference's order).
 
 A "step" = one fused bucket (one kernel launch) through the C ABI
 (bnpp_bucket_eliminate) on torch's current stream.  Roofline: algorithmic bytes
@@ -20,7 +23,9 @@ single core, on a bounded sample of the same bucket shape.
 32x32 Ising grid UAI (BASELINE config 3) through the checkpointed two-pass
 bucket tree (column-sweep order, width 32, fp32), split over the ranks by
 chain segments; wall-clock like the reference's uptime, warm (second call on
-the context, arena reused; "cold_wall_ms" = the first call, which maps it).  The reference cannot
+the context, arena reused; "cold_wall_ms" = the first call, which maps it).
+"check": P(x_t = 0) of three targets against Z(x_t = 0) / Z from conditioned
+partitions on the same context (rank 0, after the timed calls).  The reference cannot
 run this instance (min-fill width 46), so its time is bounded from below by
 n_vars x the column-sweep PR's factor-entries at the measured cpu_baseline
 rate.  "secondary": 12x12 (reference-runnable, measured reference time).
@@ -94,6 +99,17 @@ def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_or
                name, "column-sweep (width %d)" % rows if column_order else "min-fill", dtype_name),
            "wall_ms": ms, "cold_wall_ms": cold_ms, "n_gpus": world, "p_var0": marg[0],
            "max_sum_err": max(abs(sum(p) - 1.0) for p in marg.values())}
+    if rank == 0:
+        # P(x_t = 0) = Z(x_t = 0) / Z, each Z by one conditioned VE (BN::partition)
+        lz = bnpp.partition(ctx, m, {}, "mf", dt, order=order)[0]
+        tol = 1e-6 if dt == bnpp.F32 else 1e-11
+        errs = {}
+        for t in (0, (rows // 2) * cols + cols // 2, rows * cols - 1):
+            lz0 = bnpp.partition(ctx, m, {t: 0}, "mf", dt, order=order)[0]
+            errs[str(t)] = abs(10 ** (lz0 - lz) - marg[t][0])
+        rec["check"] = {"method": "P(x_t=0) vs Z(x_t=0)/Z from conditioned partitions", "abs_err": errs,
+                        "max_abs_err": max(errs.values()), "tolerance": tol,
+                        "ok": max(errs.values()) <= tol}
     ref_file = os.path.join(REPO, "profiles", "r01_ve_bench.jsonl")
     ref_ms = None
     if os.path.exists(ref_file):
@@ -199,9 +215,20 @@ def main():
     want = (m_t.double().reshape(k, S).sum(1) * f_t.double().reshape(k, k).sum(1)).sum().item()
     got = out.double().sum().item()
     ok = abs(got - want) <= (1e-4 if dt == bnpp.F32 else 1e-9) * want
+    # exact spot check: out[s*k + y] = ((0 + m[0,s] f[0,y]) + m[1,s] f[1,y]) + ... in the
+    # compute dtype, products and sums rounded one at a time like factor.cpp:131-143, 199-205
+    gs = torch.Generator(device=dev).manual_seed(99 + rank)
+    idx = torch.randint(0, S * k, (512,), generator=gs, device=dev)
+    s_i, y_i = idx // k, idx % k
+    M, F = m_t.reshape(k, S), f_t.reshape(k, k)
+    acc = torch.zeros(512, device=dev, dtype=tdt)
+    for x in range(k):
+        acc = acc + M[x, s_i] * F[x, y_i]
+    spot_ok = bool(torch.equal(out[idx], acc))
+    ok = ok and spot_ok
 
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "traffic_r01.json")
+    tpath = os.path.join(REPO, "profiles", "traffic_r02.json")   # tools/profile_bench.sh, this kernel
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
         if tj.get("k") == k and tj.get("w") == w and tj.get("dtype") == args.dtype:
@@ -235,7 +262,7 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic (U(0.5,2) potentials, seeded)",
             "config": {"workload": "potts-k%d bucket m(x,S_1..S_%d)*f(x,y)->sum_x (BASELINE config 5 restated, "
-                                   "SURVEY.md 8(d)); output split on a leading variable across ranks" % (k, w),
+                                   "SURVEY.md 8(d)); one independent bucket per rank" % (k, w),
                        "k": k, "w": w, "entries_per_gpu_step": entries, "parallelism": "bucket-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
@@ -243,10 +270,13 @@ def main():
             "cpu_baseline": cpu,
             "mar": mar,
             "checksum_ok": ok,
+            "spot_check_exact": spot_ok,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if mar and "check" in mar and not mar["check"]["ok"]:
+        ok = False
     if not ok:
         sys.exit(3)
 

@@ -219,7 +219,7 @@ Factor Factor::product(const Factor &f) const {
     auto a = upload(_values), b = upload(f._values);
     DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
     std::vector<int> av = ids(*_domain), bv = ids(*f._domain), ov = ids(*nd);
-    check(bnpp_product(ctx(), nullptr, BNPP_F64, cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
+    check(bnpp_product(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
                        bv.data(), out.p, (int)ov.size(), ov.data()),
           "product");
     std::vector<double> vals = download(out, nd->size());
@@ -233,7 +233,7 @@ Factor Factor::divide(const Factor &f) const {
     auto a = upload(_values), b = upload(f._values);
     DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
     std::vector<int> av = ids(*_domain), bv = ids(*f._domain), ov = ids(*nd);
-    check(bnpp_divide(ctx(), nullptr, BNPP_F64, cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
+    check(bnpp_divide(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
                       bv.data(), out.p, (int)ov.size(), ov.data()),
           "divide");
     std::vector<double> vals = download(out, nd->size());
@@ -248,7 +248,7 @@ Factor Factor::sum_out(const Variable *variable) const {
     auto a = upload(_values);
     DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
     std::vector<int> av = ids(*_domain), ov = ids(*nd);
-    check(bnpp_sum_out(ctx(), nullptr, BNPP_F64, cards.data(), a->p, (int)av.size(), av.data(), (int)variable->id(),
+    check(bnpp_sum_out(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), (int)variable->id(),
                        out.p, (int)ov.size(), ov.data()),
           "sum_out");
     std::vector<double> vals = download(out, nd->size());
@@ -267,7 +267,7 @@ Factor Factor::conditioning(const std::unordered_map<unsigned, unsigned> &eviden
     auto a = upload(_values);
     DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
     std::vector<int> av = ids(*_domain);
-    check(bnpp_condition(ctx(), nullptr, BNPP_F64, cards.data(), a->p, (int)av.size(), av.data(), (int)ev_vars.size(),
+    check(bnpp_condition(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), (int)ev_vars.size(),
                          ev_vars.data(), ev_vals.data(), out.p),
           "conditioning");
     std::vector<double> vals = download(out, nd->size());

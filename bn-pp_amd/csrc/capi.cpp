@@ -76,11 +76,11 @@ double now_ms() {
         return set_err(BNPP_ERR_INVALID, "unknown error");                   \
     }
 
-bool valid_scope(int ndims, const int *vars, const int *cards, int ncards_hint) {
-    (void)ncards_hint;
+// every id in [0, n_cards) with a positive cardinality, no repeats
+bool valid_scope(int ndims, const int *vars, const int *cards, int n_cards) {
     if (ndims < 0 || (ndims > 0 && !vars)) return false;
     for (int i = 0; i < ndims; ++i) {
-        if (vars[i] < 0 || cards[vars[i]] < 1) return false;
+        if (vars[i] < 0 || vars[i] >= n_cards || cards[vars[i]] < 1) return false;
         for (int j = 0; j < i; ++j)
             if (vars[j] == vars[i]) return false;
     }
@@ -383,13 +383,16 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     return BNPP_OK;
 }
 
-int64_t memory_budget(bnpp_ctx *ctx) {
+// use_cache: the caller holds ctx->cache_mu and may reuse the cached arena, so
+// its bytes count as free; a call that could not take the lock must not plan
+// against memory another call is holding
+int64_t memory_budget(bnpp_ctx *ctx, bool use_cache = false) {
     if (const char *e = std::getenv("BNPP_MEM_BUDGET_GB")) return (int64_t)(std::atof(e) * 1e9);
     if (ctx) {
         size_t fr = 0, tot = 0;
         (void)hipSetDevice(ctx->c.device);
         if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0)
-            return (int64_t)((fr + ctx->c.arena_cache_bytes) * 0.85);   // the cached arena is reusable
+            return (int64_t)((fr + (use_cache ? ctx->c.arena_cache_bytes : 0)) * 0.85);
     }
     return (int64_t)64e9;
 }
@@ -418,7 +421,7 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     }
     std::vector<Schedule> batches;
     if (n_parts < 1 || part < 0 || part >= n_parts) return set_err(BNPP_ERR_INVALID, "bad part / n_parts");
-    int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, memory_budget(ctx),
+    int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, memory_budget(ctx, use_cache),
                             batches, job->stats, part, n_parts);
     if (rc) return rc;
     const double t0 = now_ms();
@@ -604,22 +607,19 @@ int bnpp_out_scope(int n_in, const int *in_ndims, const int *const *in_vars, int
     BNPP_GUARD_END
 }
 
-int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, int n_in,
+int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, int n_in,
                           const void *const *in_tables, const int *in_ndims, const int *const *in_vars, int elim_var,
                           void *out_table, int out_ndims, const int *out_vars) {
     BNPP_GUARD_BEGIN
     if (!ctx || !cards || n_in < 1 || !in_tables || !in_ndims || !in_vars || !out_table)
         return set_err(BNPP_ERR_INVALID, "null argument");
     if (n_in > kMaxIn) return set_err(BNPP_ERR_UNSUPPORTED, "at most 8 inputs per fused call");
-    int max_var = elim_var;
-    for (int i = 0; i < n_in; ++i) {
-        for (int j = 0; j < in_ndims[i]; ++j) max_var = std::max(max_var, in_vars[i][j]);
-    }
-    for (int j = 0; j < out_ndims; ++j) max_var = std::max(max_var, out_vars[j]);
-    std::vector<int> cv(cards, cards + max_var + 1);
+    if (n_cards < 0 || elim_var >= n_cards || (out_ndims > 0 && !out_vars))
+        return set_err(BNPP_ERR_INVALID, "variable id outside cards[0, n_cards)");
     for (int i = 0; i < n_in; ++i)
-        if (!valid_scope(in_ndims[i], in_vars[i], cv.data(), 0)) return set_err(BNPP_ERR_INVALID, "bad input scope");
-    if (!valid_scope(out_ndims, out_vars, cv.data(), 0)) return set_err(BNPP_ERR_INVALID, "bad output scope");
+        if (!valid_scope(in_ndims[i], in_vars[i], cards, n_cards)) return set_err(BNPP_ERR_INVALID, "bad input scope");
+    if (!valid_scope(out_ndims, out_vars, cards, n_cards)) return set_err(BNPP_ERR_INVALID, "bad output scope");
+    std::vector<int> cv(cards, cards + n_cards);
     BucketSpec b;
     std::vector<const void *> ptrs;
     for (int i = 0; i < n_in; ++i) {
@@ -641,30 +641,26 @@ int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, const int *car
     BNPP_GUARD_END
 }
 
-int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *a, int a_ndims,
+int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *a, int a_ndims,
                  const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
                  const int *out_vars) {
     const void *tabs[2] = {a, b};
     const int nd[2] = {a_ndims, b_ndims};
     const int *vs[2] = {a_vars, b_vars};
-    return bnpp_bucket_eliminate(ctx, stream, dtype, cards, 2, tabs, nd, vs, -1, out, out_ndims, out_vars);
+    return bnpp_bucket_eliminate(ctx, stream, dtype, n_cards, cards, 2, tabs, nd, vs, -1, out, out_ndims, out_vars);
 }
 
-int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *a, int a_ndims,
+int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *a, int a_ndims,
                 const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
                 const int *out_vars) {
     BNPP_GUARD_BEGIN
     if (!ctx || !cards || !a || !b || !out || (a_ndims > 0 && !a_vars) || (b_ndims > 0 && !b_vars) ||
         (out_ndims > 0 && !out_vars))
         return set_err(BNPP_ERR_INVALID, "null argument");
-    int max_var = -1;
-    for (int j = 0; j < a_ndims; ++j) max_var = std::max(max_var, a_vars[j]);
-    for (int j = 0; j < b_ndims; ++j) max_var = std::max(max_var, b_vars[j]);
-    for (int j = 0; j < out_ndims; ++j) max_var = std::max(max_var, out_vars[j]);
-    std::vector<int> cv(cards, cards + max_var + 1);
-    if (!valid_scope(a_ndims, a_vars, cv.data(), 0) || !valid_scope(b_ndims, b_vars, cv.data(), 0))
+    if (!valid_scope(a_ndims, a_vars, cards, n_cards) || !valid_scope(b_ndims, b_vars, cards, n_cards))
         return set_err(BNPP_ERR_INVALID, "bad input scope");
-    if (!valid_scope(out_ndims, out_vars, cv.data(), 0)) return set_err(BNPP_ERR_INVALID, "bad output scope");
+    if (!valid_scope(out_ndims, out_vars, cards, n_cards)) return set_err(BNPP_ERR_INVALID, "bad output scope");
+    std::vector<int> cv(cards, cards + n_cards);
     BucketSpec bs;
     bs.in.push_back(natural_view(0, std::vector<int>(a_vars, a_vars + a_ndims), cv));
     bs.in.push_back(natural_view(1, std::vector<int>(b_vars, b_vars + b_ndims), cv));
@@ -679,26 +675,24 @@ int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const 
     BNPP_GUARD_END
 }
 
-int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
+int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *in, int ndims,
                  const int *vars, int var, void *out, int out_ndims, const int *out_vars) {
     const void *tabs[1] = {in};
-    return bnpp_bucket_eliminate(ctx, stream, dtype, cards, 1, tabs, &ndims, &vars, var, out, out_ndims, out_vars);
+    return bnpp_bucket_eliminate(ctx, stream, dtype, n_cards, cards, 1, tabs, &ndims, &vars, var, out, out_ndims, out_vars);
 }
 
-int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
+int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *in, int ndims,
                    const int *vars, int n_ev, const int *ev_vars, const int *ev_vals, void *out) {
     BNPP_GUARD_BEGIN
     if (!ctx || !cards || !in || !out || (ndims > 0 && !vars) || n_ev < 0 || (n_ev > 0 && (!ev_vars || !ev_vals)))
         return set_err(BNPP_ERR_INVALID, "null argument");
-    int max_var = 0;
-    for (int j = 0; j < ndims; ++j) max_var = std::max(max_var, vars[j]);
-    std::vector<int> cv(cards, cards + max_var + 1);
-    if (!valid_scope(ndims, vars, cv.data(), 0)) return set_err(BNPP_ERR_INVALID, "bad scope");
-    std::vector<int> ev(max_var + 1, -1);
+    if (!valid_scope(ndims, vars, cards, n_cards)) return set_err(BNPP_ERR_INVALID, "bad scope");
+    std::vector<int> cv(cards, cards + n_cards);
+    std::vector<int> ev(n_cards, -1);
     for (int i = 0; i < n_ev; ++i) {
         int v = ev_vars[i];
         if (v < 0) return set_err(BNPP_ERR_INVALID, "bad evidence variable");
-        if (v > max_var) continue;                          // not in this factor's scope
+        if (v >= n_cards) continue;                         // not in this factor's scope
         if (ev_vals[i] < 0 || ev_vals[i] >= cv[v]) return set_err(BNPP_ERR_INVALID, "evidence value out of range");
         ev[v] = ev_vals[i];
     }

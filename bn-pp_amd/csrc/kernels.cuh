@@ -387,7 +387,14 @@ __device__ __forceinline__ void flush_max(T lmax, TableMeta *meta, int out_table
     if (threadIdx.x == 0 && (flags & kTrackMax)) {
         T m = red[0];
         for (int i = 1; i < kBlock / 64; ++i) m = red[i] > m ? red[i] : m;
-        if (m > T(0)) atomicMax(reinterpret_cast<typename FBits<T>::U *>(&meta[out_table].maxbits), FBits<T>::bits(m));
+        // skip the atomic when the table's max already covers this block: with
+        // one workgroup per block, hundreds of thousands of same-address
+        // atomics would serialise (~12 ns each); a stale read only costs a
+        // needless atomic
+        using U = typename FBits<T>::U;
+        U *mb = reinterpret_cast<U *>(&meta[out_table].maxbits);
+        const U mine = FBits<T>::bits(m);
+        if (m > T(0) && __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mine) atomicMax(mb, mine);
     }
     __syncthreads();
 }

@@ -51,11 +51,11 @@ _SIGS = {
     "bnpp_memcpy_d2h": (_I, [_P, _P, _P, C.c_size_t]),
     "bnpp_synchronize": (_I, [_P, _P]),
     "bnpp_out_scope": (_I, [_I, _IP, C.POINTER(_IP), _I, _I, _IP, _IP]),
-    "bnpp_bucket_eliminate": (_I, [_P, _P, _I, _IP, _I, C.POINTER(_P), _IP, C.POINTER(_IP), _I, _P, _I, _IP]),
-    "bnpp_product": (_I, [_P, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP]),
-    "bnpp_divide": (_I, [_P, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP]),
-    "bnpp_sum_out": (_I, [_P, _P, _I, _IP, _P, _I, _IP, _I, _P, _I, _IP]),
-    "bnpp_condition": (_I, [_P, _P, _I, _IP, _P, _I, _IP, _I, _IP, _IP, _P]),
+    "bnpp_bucket_eliminate": (_I, [_P, _P, _I, _I, _IP, _I, C.POINTER(_P), _IP, C.POINTER(_IP), _I, _P, _I, _IP]),
+    "bnpp_product": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP]),
+    "bnpp_divide": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP]),
+    "bnpp_sum_out": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _I, _P, _I, _IP]),
+    "bnpp_condition": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _I, _IP, _IP, _P]),
     "bnpp_model_load_uai": (_I, [C.c_char_p, C.POINTER(_P)]),
     "bnpp_model_from_arrays": (_I, [_I, _I, _IP, _I, _IP, _IP, _DP, C.POINTER(_P)]),
     "bnpp_model_free": (_I, [_P]),
@@ -398,7 +398,7 @@ def bucket_eliminate(ctx: Context, dtype: int, cards: Sequence[int], tables: Seq
     arrs = [_ints(s) for s in scopes]
     ptrs = (_IP * len(arrs))(*[C.cast(a, _IP) for a in arrs])
     tabs = (_P * len(tables))(*[_P(t) for t in tables])
-    _check(_lib.bnpp_bucket_eliminate(ctx.handle, _P(stream) if stream else None, dtype, _ints(cards), len(tables),
+    _check(_lib.bnpp_bucket_eliminate(ctx.handle, _P(stream) if stream else None, dtype, len(cards), _ints(cards), len(tables),
                                       tabs, _ints([len(s) for s in scopes]), ptrs, elim, _P(out), len(out_vars),
                                       _ints(out_vars)), "bnpp_bucket_eliminate")
 
@@ -407,7 +407,7 @@ def divide(ctx: Context, dtype: int, cards: Sequence[int], a: int, a_scope: Sequ
            b_scope: Sequence[int], out: int, out_vars: Sequence[int], stream: Optional[int] = None) -> None:
     """Factor::divide (factor.cpp:149-180) on caller-owned device buffers:
     out = a / b over the union scope (out_vars in any order of it)."""
-    _check(_lib.bnpp_divide(ctx.handle, _P(stream) if stream else None, dtype, _ints(cards), _P(a), len(a_scope),
+    _check(_lib.bnpp_divide(ctx.handle, _P(stream) if stream else None, dtype, len(cards), _ints(cards), _P(a), len(a_scope),
                             _ints(a_scope), _P(b), len(b_scope), _ints(b_scope), _P(out), len(out_vars),
                             _ints(out_vars)), "bnpp_divide")
 
@@ -415,5 +415,5 @@ def divide(ctx: Context, dtype: int, cards: Sequence[int], a: int, a_scope: Sequ
 def condition(ctx: Context, dtype: int, cards: Sequence[int], table: int, scope: Sequence[int],
               evidence: Dict[int, int], out: int, stream: Optional[int] = None) -> None:
     n, ev_v, ev_x = _ev(evidence)
-    _check(_lib.bnpp_condition(ctx.handle, _P(stream) if stream else None, dtype, _ints(cards), _P(table), len(scope),
+    _check(_lib.bnpp_condition(ctx.handle, _P(stream) if stream else None, dtype, len(cards), _ints(cards), _P(table), len(scope),
                                _ints(scope), n, ev_v, ev_x, _P(out)), "bnpp_condition")

@@ -14,7 +14,8 @@
  *     last failure on the calling thread.
  *   - Tables are row-major over their scope with the LAST variable fastest
  *     (domain.cpp:15-26).  Scopes are arrays of variable ids; `cards` is indexed
- *     by variable id.
+ *     by variable id and holds n_cards entries: an id outside [0, n_cards)
+ *     anywhere in a call is BNPP_ERR_INVALID (the array is never read past).
  *   - Device tables passed to the single-op calls are caller-owned device
  *     buffers (bnpp_malloc, hipMalloc or a torch tensor's data_ptr); the engine
  *     never frees them.  `stream` is a hipStream_t (NULL: the context stream).
@@ -36,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BNPP_VERSION 100
+#define BNPP_VERSION 200   /* 200: single ops take n_cards (the length of cards) */
 
 enum bnpp_status {
     BNPP_OK = 0,
@@ -87,29 +88,29 @@ int bnpp_out_scope(int n_in, const int *in_ndims, const int *const *in_vars, int
  * out_vars must be the layout from bnpp_out_scope (or any permutation of it).
  * 1 <= n_in <= 8; elim_var < 0 means no summation; elim_var absent from every
  * input makes it a copy (factor.cpp:185-188). */
-int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, int n_in,
+int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, int n_in,
                           const void *const *in_tables, const int *in_ndims, const int *const *in_vars,
                           int elim_var, void *out_table, int out_ndims, const int *out_vars);
 
 /* Factor::product (factor.cpp:117-147; factor.hh:35) */
-int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *a, int a_ndims,
+int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *a, int a_ndims,
                  const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
                  const int *out_vars);
 
 /* Factor::divide (factor.cpp:149-180; factor.hh:36): out = a / b over the
  * union scope (out_vars: any order of it).  The reference asserts on a zero
  * divisor (factor.cpp:165); here it yields inf / nan in that entry. */
-int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *a, int a_ndims,
+int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *a, int a_ndims,
                 const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
                 const int *out_vars);
 
 /* Factor::sum_out (factor.cpp:182-212; factor.hh:34) */
-int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
+int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *in, int ndims,
                  const int *vars, int var, void *out, int out_ndims, const int *out_vars);
 
 /* Factor::conditioning (factor.cpp:214-242; factor.hh:38): out scope = vars minus
  * evidence vars, order preserved (domain.cpp:74-90) */
-int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, const int *cards, const void *in, int ndims,
+int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *in, int ndims,
                    const int *vars, int n_ev, const int *ev_vars, const int *ev_vals, void *out);
 
 /* ------------------------------------------------------ models (host) */

@@ -323,6 +323,17 @@ def test_invalid_shapes_rejected(ctx):
     assert e.value.status == bnpp.ERR_INVALID
     with pytest.raises(bnpp.BnppError):            # more than 8 inputs
         bnpp.bucket_eliminate(ctx, bnpp.F64, [2], [a.data_ptr()] * 9, [[0]] * 9, -1, out.data_ptr(), [0])
+    # variable ids outside cards[0, n_cards) are rejected before cards is read
+    for scope, elim, ov in (([2], -1, [2]), ([0], 5, [0]), ([-1], -1, [-1]), ([0], -1, [3])):
+        with pytest.raises(bnpp.BnppError) as e:
+            bnpp.bucket_eliminate(ctx, bnpp.F64, [2, 2], [a.data_ptr()], [scope], elim, out.data_ptr(), ov)
+        assert e.value.status == bnpp.ERR_INVALID, (scope, elim, ov)
+    with pytest.raises(bnpp.BnppError) as e:
+        bnpp.divide(ctx, bnpp.F64, [2], a.data_ptr(), [0], a.data_ptr(), [1], out.data_ptr(), [0, 1])
+    assert e.value.status == bnpp.ERR_INVALID
+    with pytest.raises(bnpp.BnppError) as e:
+        bnpp.condition(ctx, bnpp.F64, [2], a.data_ptr(), [4], {}, out.data_ptr())
+    assert e.value.status == bnpp.ERR_INVALID
 
 
 # ----------------------------------------------------------- whole VE runs
