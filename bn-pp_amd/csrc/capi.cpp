@@ -104,6 +104,11 @@ int run_single(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &c
     a.d.dim_off = 0;
     for (size_t i = 0; i < in_ptrs.size(); ++i) a.meta[i].ptr = const_cast<void *>(in_ptrs[i]);
     a.meta[in_ptrs.size()].ptr = out;
+    if (a.d.big >= 0) {
+        const int eb = dtype == BNPP_F32 ? 4 : 8;
+        a.big_ptr = static_cast<const unsigned char *>(in_ptrs[a.d.big]) + a.d.in_base[a.d.big] * eb;
+        a.big_es = a.d.elim_stride[a.d.big];
+    }
     hipError_t e = hipSetDevice(ctx->c.device);
     if (e == hipSuccess) e = launch_single(dtype == BNPP_F32, a, ctx->c.max_grid, pick_stream(ctx, stream));
     if (e != hipSuccess) return set_err(BNPP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));

@@ -19,6 +19,10 @@ hipError_t launch_level(int is_f32, int variant, const BucketDesc *descs, int n_
 // no rescaling): the exact Factor::product / sum_out / conditioning semantics.
 constexpr int kMaxPool = 320;   // dims-pool words that fit the kernel-argument segment
 struct SingleArgs {
+    // slab form: the big input's first entry and summed-variable stride,
+    // resolved on the host so the kernel's first loads wait on one kernarg read
+    const void *big_ptr;
+    int64_t big_es;
     BucketDesc d;
     TableMeta meta[kMaxIn + 1];  // inputs 0..n_in-1, output at index n_in
     int64_t pool[kMaxPool];

@@ -116,8 +116,7 @@ __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs ar
     if (t >= d.n_tiles) return;
     const int big = d.big;
     T m[K][V];
-    slab_load_big<T, K, C0, V, true>(static_cast<const T *>(a.meta[big].ptr) + d.in_base[big] + t * V,
-                                     d.elim_stride[big], m);
+    slab_load_big<T, K, C0, V, true>(static_cast<const T *>(a.big_ptr) + t * V, a.big_es, m);
     T acc[ST::N];
     ST::compute(m, big, d.n_in, [&](int i, T (&g)[K][C0]) {
         ST::load_small(static_cast<const T *>(a.meta[i].ptr) + d.in_base[i], d.elim_stride[i], slab_sy(d, a.pool, i), g);
