@@ -20,6 +20,8 @@
 namespace bnpp {
 
 constexpr int kMaxIn = 8;          // inputs per fused launch; longer chains are split
+constexpr int kMaxDescIn = 9;      // descriptor slots: a fused run of 8 buckets has 8 G tables + the message
+constexpr int kSplitRowsHost = 64; // rest entries per workgroup of the split chain forms (chainsplit.cuh)
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 
 // One per table (source factor or message), resident in device memory.
@@ -54,16 +56,16 @@ struct BucketDesc {
     int64_t tdiv0[2], tdiv1[2];     // divisors card0/v1 and card1/v2 (dim header, magic)
     int32_t n_in, n_dims, k, v1, v2;// k = card of the summed variable (1: pure product)
     int32_t out_table, flags;
-    int32_t in_table[kMaxIn];
-    int64_t in_base[kMaxIn];        // evidence offset of each view
-    int64_t elim_stride[kMaxIn];    // stride of the summed variable in each view (0: absent)
+    int32_t in_table[kMaxDescIn];
+    int64_t in_base[kMaxDescIn];        // evidence offset of each view
+    int64_t elim_stride[kMaxDescIn];    // stride of the summed variable in each view (0: absent)
     int64_t dim_off;                // offset into the dims pool
     // stream form (big >= 0): input `big` is read from HBM with loads of class
     // bcls; every other input is copied whole into LDS once per workgroup
     int32_t big, bcls;
     int32_t small_elems;            // LDS elements for the small inputs
-    int32_t in_lds_off[kMaxIn];     // element offset of each small input in LDS
-    int32_t in_span[kMaxIn];        // elements of each small input's reachable range
+    int32_t in_lds_off[kMaxDescIn];     // element offset of each small input in LDS
+    int32_t in_span[kMaxDescIn];        // elements of each small input's reachable range
     // chain form (chain != 0): F consecutive buckets of a sweep fused in
     // registers; chain = F | gmask << 8 | form << 16 | dep << 20 (ChainForm, ChainDep)
     int32_t chain, chain_pad;
@@ -113,7 +115,11 @@ __host__ __device__ constexpr int slab_key(int k, int c0, int v) { return 16384 
 //   kChainFwdV: kChainFwd with V rest entries per thread (vector slab loads,
 //              rows of V * K^F entries); short runs, where one entry per
 //              thread leaves the kernel issue-bound
-enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2, kChainSum = 3, kChainFwdV = 4 };
+//   kChainFwdS / kChainBwdS: the forward / backward layouts with the 2^F table
+//              of one rest entry split over 2^(F-4) waves (chainsplit.cuh;
+//              K = 2, fp32, F = 5..8), one workgroup per 64 rest entries
+enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2, kChainSum = 3, kChainFwdV = 4, kChainFwdS = 5, kChainBwdS = 6 };
+__host__ __device__ inline bool chain_split_form(int form) { return form == kChainFwdS || form == kChainBwdS; }
 // Which slots G_j depends on besides its own (x_j, n_j): the next slot (j+1,
 // e.g. a forward sweep's vertical factor), the previous one (j-1, backward),
 // or any (every G value of a bucket fetched separately; small tables only).

@@ -100,7 +100,7 @@ __device__ __forceinline__ void chain_load_state(ChainState<F> &c, const BucketD
     c.big = meta[d.in_table[0]].ptr;
     c.out = meta[d.out_table].ptr;
     int64_t e_sum = 0, x_sum = 0;
-    for (int i = 0; i < kMaxIn; ++i) {
+    for (int i = 0; i < kMaxDescIn; ++i) {
         if (i >= d.n_in) break;
         const TableMeta &mi = meta[d.in_table[i]];
         const int e = FBits<T>::exponent(mi.maxbits);
@@ -118,7 +118,7 @@ __device__ __forceinline__ void chain_load_state(ChainState<F> &c, const BucketD
 template <typename T>
 __device__ __forceinline__ int64_t chain_exp2(const BucketDesc &d, TableMeta *meta) {
     int64_t x_sum = 0;
-    for (int i = 0; i < kMaxIn; ++i) {
+    for (int i = 0; i < kMaxDescIn; ++i) {
         if (i >= d.n_in) break;
         const TableMeta &mi = meta[d.in_table[i]];
         x_sum += mi.exp2 + ((d.flags & kScale) ? FBits<T>::exponent(mi.maxbits) : 0);
@@ -130,7 +130,7 @@ __device__ __forceinline__ int64_t chain_exp2(const BucketDesc &d, TableMeta *me
 template <typename T>
 __device__ __forceinline__ void chain_stage(const BucketDesc &d, TableMeta *meta, T *small) {
     __syncthreads();
-    for (int i = 1; i < kMaxIn; ++i) {
+    for (int i = 1; i < kMaxDescIn; ++i) {
         if (i >= d.n_in) break;
         const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
         const int off = d.in_lds_off[i], span = d.in_span[i];

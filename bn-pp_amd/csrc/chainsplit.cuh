@@ -1,0 +1,436 @@
+// Split chain runs (gfx950): F = 5..8 consecutive sweep buckets of a binary
+// (K = 2) fp32 message fused in one pass, the 2^F-entry table of one rest
+// entry spread over W = 2^(F-4) waves of one workgroup (16 entries per lane).
+//
+// Same arithmetic as chain.cuh (one thread per rest entry, all 2^F entries in
+// its registers), which caps a run at 6 buckets (64 registers of table, 3 waves
+// per SIMD).  Here a workgroup owns 64 consecutive rest entries (one per lane):
+//   phase 1  wave w holds the 16 assignments of slots 0-3 whose slots 4..F-1
+//            are w, and runs buckets 0-3 in registers;
+//   exchange the 64 x 2^F table goes through LDS (one barrier);
+//   phase 2  wave w holds new digits 0-3 in its group and slots 4..F-1, and
+//            runs buckets 4..F-1 in registers.
+// Every bucket is the reference's arithmetic in the reference's order (p = G *
+// m; acc = 0; acc += p over x = 0, 1: factor.cpp:131-143, 199-205), so the
+// result is the unfused one's up to the power-of-two scale applied at the end.
+// A G value depends on at most one other slot (ChainDep next / prev); a slot
+// outside the wave's register group has a wave-uniform digit.
+//
+// Forward form (summed variables the input's slowest): 16 slab loads per lane
+// (256 B per slab per wave-instruction); the wave's 16 outputs of a row are
+// contiguous, rows (2^F entries) leave through an LDS image as 4 KiB per wave.
+// Backward form (summed variables the input's fastest): the 64 input rows come
+// in by 16-B loads through the LDS image; 16 slab stores per lane.
+// Persistent grid (16 waves per CU), next tile's loads issued before the
+// current tile is computed (tools/chainbw.hip: the 8-bucket split pattern
+// moves 5.4-5.5 TB/s against 5.1-5.3 for 6-bucket runs one thread per rest entry).
+#pragma once
+#include "chain.cuh"
+
+namespace bnpp {
+
+constexpr int kSplitRows = kSplitRowsHost;   // rest entries per workgroup (one per lane)
+
+__host__ __device__ constexpr int split_waves(int f) { return 1 << (f - 4); }
+// LDS bytes: max(exchange table, row image) + the G tables
+__host__ __device__ constexpr int split_img_bytes(int f) {
+    return kSplitRows * ((1 << f) * 4 + 16) > kSplitRows * (1 << f) * 4 ? kSplitRows * ((1 << f) * 4 + 16)
+                                                                         : kSplitRows * (1 << f) * 4;
+}
+
+// One bucket J (slot J, 0-3 in phase 1, 4..F-1 in phase 2) on the lane's 16
+// entries.  The local index e holds the local slots' digits; digit(e, p) gives
+// any slot's digit for entry e (local ones from e, the others wave-uniform).
+template <int F, int PH, int J, int DEP, typename Digit>
+__device__ __forceinline__ void split_step(float (&t)[16], const float *small, int32_t gb, int32_t gsj, int32_t gsq,
+                                           int32_t gsn, Digit &&digit) {
+    // place of slot J in the local index
+    constexpr int PJ = PH == 1 ? (8 >> J) : (1 << (F - 1 - J));
+    constexpr int Q = DEP == kDepNext ? J + 1 : J - 1;
+    constexpr bool HASQ = Q >= 0 && Q < F;
+    // the bucket's G values, fetched once: [q][n][x] (q: digit of slot Q)
+    constexpr int NQ = HASQ ? 2 : 1;
+    float g[NQ][2][2];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int32_t go = gb + (HASQ ? q * gsq : 0);
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int x = 0; x < 2; ++x) g[q][n][x] = small[go + x * gsj + n * gsn];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        if (e & PJ) continue;
+        const int q = HASQ ? digit(e, HASQ ? Q : 0) : 0;    // constant for local slots
+        const float g00 = NQ == 2 && q ? g[NQ - 1][0][0] : g[0][0][0];
+        const float g10 = NQ == 2 && q ? g[NQ - 1][0][1] : g[0][0][1];
+        const float g01 = NQ == 2 && q ? g[NQ - 1][1][0] : g[0][1][0];
+        const float g11 = NQ == 2 && q ? g[NQ - 1][1][1] : g[0][1][1];
+        const float m0 = t[e], m1 = t[e | PJ];
+        float a0 = 0.f, a1 = 0.f;
+        a0 = a0 + g00 * m0;
+        a0 = a0 + g10 * m1;
+        a1 = a1 + g01 * m0;
+        a1 = a1 + g11 * m1;
+        t[e] = a0;
+        t[e | PJ] = a1;
+    }
+}
+
+// What a split run needs of its descriptor, kept small (uniform registers):
+// the slab offsets of the wave's 16 phase-1 entries (forward), the output
+// strides of its 16 phase-2 entries (backward), and per bucket the strides of
+// G_j along x_j, along the dependency slot and along n_j.
+template <int F, int DEP>
+struct SplitState {
+    const float *big;
+    float *out;
+    const int64_t *dims;
+    int64_t n_tiles, in_base, t0h, t0m;
+    int n_dims, gmask, flags, neg_e;
+    int64_t is4[4], isw;          // input stride of slots 0-3; slots 4.. of this wave
+    int64_t osl[4], osw;          // output stride of the 4 phase-2 local slots; the wave's other slots
+    int32_t glds[F], gsj[F], gsq[F], gsn[F];
+};
+
+template <int F, int DEP>
+__device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const BucketDesc &d, const int64_t *pool,
+                                                 TableMeta *meta, int w) {
+    constexpr int HB = 8 - F;
+    c.dims = pool;
+    c.n_dims = d.n_dims;
+    c.n_tiles = d.n_tiles;
+    c.t0h = d.tdiv0[0];
+    c.t0m = d.tdiv0[1];
+    c.gmask = (d.chain >> 8) & 0xff;
+    c.flags = d.flags;
+    c.in_base = d.in_base[0];
+    const int64_t *sl = pool + (int64_t)d.n_dims * (4 + F);
+    c.isw = 0;
+    c.osw = 0;
+#pragma unroll
+    for (int p = 0; p < F; ++p) {
+        const int64_t is = sl[2 * p], os = sl[2 * p + 1];
+        if (p < 4) c.is4[p] = is;
+        else c.isw += (int64_t)((w >> (F - 1 - p)) & 1) * is;
+        // phase 2: local bits of e are slots 4-HB .. F-1 (MSB first); slots
+        // below 4-HB carry the wave's digits (cgrp = w << HB | h, slot p = bit 3-p)
+        if (p >= 4 - HB) c.osl[p - (4 - HB)] = os;
+        else c.osw += (int64_t)((((w << HB) >> (3 - p)) & 1)) * os;
+    }
+    const int64_t *st = sl + 2 * F;
+    int gi = 1;
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+        const int q = DEP == kDepNext ? j + 1 : j - 1;
+        c.gsj[j] = (int32_t)st[j * (F + 1) + j];
+        c.gsq[j] = q >= 0 && q < F ? (int32_t)st[j * (F + 1) + q] : 0;
+        c.gsn[j] = (int32_t)st[j * (F + 1) + F];
+        const bool on = (c.gmask >> j) & 1;
+        c.glds[j] = on ? d.in_lds_off[gi] : 0;
+        gi += on ? 1 : 0;
+    }
+    c.big = static_cast<const float *>(meta[d.in_table[0]].ptr);
+    c.out = static_cast<float *>(meta[d.out_table].ptr);
+    int64_t e_sum = 0;
+    for (int i = 0; i < kMaxDescIn; ++i) {
+        if (i >= d.n_in) break;
+        if (d.flags & kScale) e_sum += FBits<float>::exponent(meta[d.in_table[i]].maxbits);
+    }
+    c.neg_e = (int)(-e_sum);
+}
+
+#ifndef BNPP_SPLIT_WAVES
+#define BNPP_SPLIT_WAVES 0     // waves per SIMD the register allocation must allow (0: compiler's choice)
+#endif
+// workgroup barrier for the LDS exchange only: waits for this wave's LDS
+// operations, not for its global loads and stores (__syncthreads would wait
+// vmcnt(0) and drain the next tile's prefetched loads)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Persistent workgroups walk the level's tiles (64 rest entries each) grid-
+// stride; the next tile's message loads are issued before the current tile is
+// computed, so HBM stays busy through the exchange barriers and the stores.
+template <int F, int FORM, int DEP>
+__global__ __launch_bounds__(64 * (1 << (F - 4))) __attribute__((amdgpu_waves_per_eu(BNPP_SPLIT_WAVES > 0 ? BNPP_SPLIT_WAVES : 1)))
+void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const int64_t *__restrict__ pool,
+                        TableMeta *__restrict__ meta, int64_t total_vblocks) {
+    using T = float;
+    constexpr int W = split_waves(F);
+    constexpr int N = 1 << F;
+    constexpr int ROWB = N * 4 + 16;                       // image row stride (bytes)
+    constexpr int HB = 8 - F;                              // phase 2: bits of h (n-digits 0-3 local)
+    constexpr int SB = F - 4;                              // phase 2: bits of the slot combo (slots 4..F-1)
+    constexpr int RPW = kSplitRows / W;                    // backward: input rows loaded per wave
+    constexpr int CPR = N / 4;                             // backward: 16-B chunks per row
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    T *red = reinterpret_cast<T *>(dyn);
+    unsigned char *img = dyn + kRedBytes;
+    T *xch = reinterpret_cast<T *>(img);
+    T *small = reinterpret_cast<T *>(dyn + kRedBytes + split_img_bytes(F));
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // digit of slot p (4 <= p < F) in phase 1: bit (F-1-p) of w
+    auto wdig = [&](int p) { return (w >> (F - 1 - p)) & 1; };
+
+    int cur = -1;
+    int64_t cur_begin = 0, cur_end = 0;
+    SplitState<F, DEP> c;
+    T lmax = T(0);
+
+    // bucket of virtual block vb: state, published exponent, G tables in LDS
+    auto setup = [&](int64_t vb) {
+        const int bi = n_desc == 1 ? 0 : find_bucket(descs, n_desc, vb);
+        const BucketDesc &d = descs[bi];
+        cur = bi;
+        cur_begin = d.vblk_begin;
+        cur_end = bi + 1 < n_desc ? descs[bi + 1].vblk_begin : total_vblocks;
+        split_load_state<F, DEP>(c, d, pool + d.dim_off, meta, w);
+        if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta);
+        lds_barrier();                                     // the previous bucket's tables are no longer read
+        for (int i = 1; i < kMaxDescIn; ++i) {
+            if (i >= d.n_in) break;
+            const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
+            const int off = d.in_lds_off[i], span = d.in_span[i];
+            for (int e = threadIdx.x; e < span; e += 64 * W) small[off + e] = gload(src + e);
+        }
+        lds_barrier();
+    };
+    // rest entry of this lane in tile vb: input / output offsets, G offsets
+    auto decode = [&](int64_t vb, int64_t &in_off, int64_t &out_off, int32_t (&gb)[F]) {
+        const int64_t tid = (vb - cur_begin) * kSplitRows + lane;
+        const int row = 4 + F;
+        const int64_t *dp = c.dims;
+        uint64_t q, r;
+        divmod_dim((uint64_t)tid, c.t0h, c.t0m, q, r);
+        in_off = c.in_base + (int64_t)r * dp[2];
+        out_off = (int64_t)r * dp[3];
+#pragma unroll
+        for (int j = 0; j < F; ++j) gb[j] = c.glds[j] + (int32_t)r * (int32_t)dp[4 + j];
+        uint64_t rem = q;
+        dp += row;
+        for (int dd = 1; dd < c.n_dims; ++dd) {
+            uint64_t qq, rr;
+            divmod_dim(rem, dp[0], dp[1], qq, rr);
+            in_off += (int64_t)rr * dp[2];
+            out_off += (int64_t)rr * dp[3];
+#pragma unroll
+            for (int j = 0; j < F; ++j) gb[j] += (int32_t)rr * (int32_t)dp[4 + j];
+            rem = qq;
+            dp += row;
+        }
+    };
+    // the tile's message loads (16 values per lane)
+    auto issue = [&](int64_t in_off, float (&rg)[16]) {
+        if constexpr (FORM == kChainFwd) {
+            // slab of assignment (slots 0-3 = e, slots 4.. = w): uniform base + 32-bit lane offset
+            const int64_t w0 = readfirstlane64(in_off);
+            const uint32_t lob = (uint32_t)((in_off - w0) * 4);
+            const T *wb = c.big + w0 + c.isw;              // uniform
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                int64_t o = 0;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) o += (int64_t)((e >> (3 - p)) & 1) * c.is4[p];
+                const T *sp = wb + o;                      // uniform slab base
+                rg[e] = gload(reinterpret_cast<const T *>(reinterpret_cast<const char *>(sp) + lob));
+            }
+        } else {
+            // 64 input rows of N contiguous values (slot 0 fastest): wave w loads
+            // its RPW rows with 16-B loads (4 per lane)
+            const T *big = c.big;
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int q = it * 64 + lane;
+                const int rw = w * RPW + q / CPR, ch = q % CPR;
+                const int64_t ro = __shfl(in_off, rw, 64);  // row rw's input offset (held by lane rw)
+                const vec_t<T, 4> v = vload<4, kNtLoad, true>(big + ro + 4 * ch);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) rg[4 * it + k] = v[k];
+            }
+        }
+    };
+    auto flush = [&]() {
+        const T wm = wave_max(lmax);
+        lds_barrier();
+        if (lane == 0) red[w] = wm;
+        lds_barrier();
+        if (threadIdx.x == 0 && (c.flags & kTrackMax)) {
+            T m = red[0];
+            for (int i = 1; i < W; ++i) m = red[i] > m ? red[i] : m;
+            using U = typename FBits<T>::U;
+            U *mb = reinterpret_cast<U *>(&meta[descs[cur].out_table].maxbits);
+            const U mine = FBits<T>::bits(m);
+            if (m > T(0) && __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mine) atomicMax(mb, mine);
+        }
+        lmax = T(0);
+    };
+
+    // one tile: the 16 values per lane in t, this lane's rest entry decoded
+    auto run_tile = [&](float (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
+        lds_barrier();                                     // the previous tile's LDS reads are done
+        if constexpr (FORM == kChainBwd) {
+            // rows through the image, then this lane's 16 entries (slots 4.. = w)
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int q = it * 64 + lane;
+                const int rw = w * RPW + q / CPR, ch = q % CPR;
+                *reinterpret_cast<vec_t<T, 4> *>(img + rw * ROWB + 16 * ch) =
+                    vec_t<T, 4>{t[4 * it], t[4 * it + 1], t[4 * it + 2], t[4 * it + 3]};
+            }
+            lds_barrier();
+            int fixed = 0;
+#pragma unroll
+            for (int p = 4; p < F; ++p) fixed += wdig(p) << p;
+            // local index e: slot 0 = bit 3 ... slot 3 = bit 0; row position: slot p at 2^p
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int pos = fixed + (((e >> 3) & 1) | (((e >> 2) & 1) << 1) | (((e >> 1) & 1) << 2) | ((e & 1) << 3));
+                t[e] = *reinterpret_cast<const T *>(img + lane * ROWB + 4 * pos);
+            }
+            lds_barrier();                                 // the image (aliased by the exchange) has been read
+        }
+
+        // phase 1: buckets 0-3 (other slots: local bits of e, slots >= 4 from w)
+        auto dig1 = [&](int e, int p) { return p < 4 ? (e >> (3 - p)) & 1 : wdig(p); };
+        static_for<4>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            split_step<F, 1, j, DEP>(t, small, gb[j], c.gsj[j], c.gsq[j], c.gsn[j], dig1);
+        });
+        // exchange: entry (n-digits 0-3 = e, slots 4.. = w) -> xch[(w * 16 + e) * 64 + lane]
+#pragma unroll
+        for (int e = 0; e < 16; ++e) xch[(w * 16 + e) * 64 + lane] = t[e];
+        lds_barrier();
+        // phase 2: local e = h << SB | sc; n-digits 0-3 = cgrp = w << HB | h; slots 4.. = sc
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int h = e >> SB, sc = e & ((1 << SB) - 1);
+            t[e] = xch[(sc * 16 + ((w << HB) | h)) * 64 + lane];
+        }
+        auto dig2 = [&](int e, int p) {
+            if (p >= 4) return (e >> (F - 1 - p)) & 1;
+            const int cg = (w << HB) | (e >> SB);
+            return (cg >> (3 - p)) & 1;
+        };
+        static_for<F - 4>([&](auto jc) {
+            constexpr int j = 4 + decltype(jc)::value;
+            split_step<F, 2, j, DEP>(t, small, gb[j], c.gsj[j], c.gsq[j], c.gsn[j], dig2);
+        });
+        if (c.flags & kScale) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) t[e] = ldexp_t(t[e], c.neg_e);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) lmax = t[e] > lmax ? t[e] : lmax;
+
+        if constexpr (FORM == kChainFwd) {
+            // row position of entry e: w * 16 + e (slot 0 most significant)
+            lds_barrier();                                 // every wave has read the exchange table
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4)
+                *reinterpret_cast<vec_t<T, 4> *>(img + lane * ROWB + 4 * (w * 16 + 4 * c4)) =
+                    vec_t<T, 4>{t[4 * c4], t[4 * c4 + 1], t[4 * c4 + 2], t[4 * c4 + 3]};
+            lds_barrier();
+            // the 64 rows are one contiguous block of 64 * N entries (planner-checked):
+            // wave w stores its 4 KiB share, 1 KiB per instruction
+            T *out = c.out + __shfl(out_off, 0, 64);
+            // (tiles are whole: the planner requires rest dim 0 to be a multiple of 64)
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int q = w * 256 + it * 64 + lane;    // 16-B chunk within the block
+                const int rw = q / (N / 4), ch = q % (N / 4);
+                const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4> *>(img + rw * ROWB + 16 * ch);
+                vstore<4, kNtStore, true>(out + 4 * (int64_t)q, v);
+            }
+        } else {
+            // slab stores: entry e has n-digits 0-3 = (w << HB | h), slots 4.. = sc
+            {
+                const int64_t w0 = readfirstlane64(out_off);
+                const uint32_t lob = (uint32_t)((out_off - w0) * 4);
+                T *wb = c.out + w0 + c.osw;                // uniform
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    int64_t o = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) o += (int64_t)((e >> (3 - b)) & 1) * c.osl[b];
+                    T *dst = reinterpret_cast<T *>(reinterpret_cast<char *>(wb + o) + lob);
+                    store_n<T, 1, kNtStore, true>(dst, &t[e]);
+                }
+            }
+        }
+    };
+
+    int64_t vb = blockIdx.x;
+    if (vb >= total_vblocks) return;
+    setup(vb);
+    float rg[16];
+    int64_t in_off, out_off;
+    int32_t gb[F];
+    if (n_desc == 1) {
+        // one bucket: the next tile's loads are issued (unconditionally: the
+        // last tile is re-read rather than branching, so the wait counts stay
+        // static) before the current tile is computed
+        decode(vb, in_off, out_off, gb);
+        issue(in_off, rg);
+        while (true) {
+            float t[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) t[e] = rg[e];
+            const int64_t vbn = vb + gridDim.x;
+            decode(vbn < total_vblocks ? vbn : total_vblocks - 1, in_off, out_off, gb);
+            issue(in_off, rg);
+            decode(vb, in_off, out_off, gb);
+            run_tile(t, out_off, gb);
+            vb = vbn;
+            if (vb >= total_vblocks) break;
+        }
+    } else {
+        while (true) {
+            float t[16];
+            decode(vb, in_off, out_off, gb);
+            issue(in_off, t);
+            run_tile(t, out_off, gb);
+            const int64_t vbn = vb + gridDim.x;
+            if (vbn >= total_vblocks) break;
+            if (vbn >= cur_end) {                          // the next tile is in another bucket of the level
+                flush();
+                setup(vbn);
+            }
+            vb = vbn;
+        }
+    }
+    flush();
+}
+
+#ifndef BNPP_SPLIT_WAVES_PER_CU
+#define BNPP_SPLIT_WAVES_PER_CU 16     // resident waves per CU the persistent grid is sized for
+#endif
+template <int F, int FORM, int DEP>
+static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_t stream) {
+    const size_t shm = kRedBytes + split_img_bytes(F) + (size_t)small_elems * sizeof(float);
+    static const hipError_t attr = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    const int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
+    const int64_t grid = a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
+    hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP>), dim3((unsigned)grid), dim3(64 * split_waves(F)), shm,
+                       stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
+    return hipGetLastError();
+}
+
+// forms kChainFwdS / kChainBwdS (bnpp_device.h), K = 2, F = 5..8, dep next / prev
+#define BNPP_CASE_CHAIN_SPLIT(F, FORM, KFORM, DEP) \
+    case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F: return go_chain_split<F, KFORM, DEP>(a, small_elems, stream);
+#define BNPP_CASE_CHAIN_SPLIT_OK(F, FORM, KFORM, DEP) case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F: return true;
+#define BNPP_CHAIN_SPLIT_FD(X, F) X(F, 5, kChainFwd, 0) X(F, 5, kChainFwd, 1) X(F, 6, kChainBwd, 0) X(F, 6, kChainBwd, 1)
+#define BNPP_CHAIN_SPLIT(X) BNPP_CHAIN_SPLIT_FD(X, 5) BNPP_CHAIN_SPLIT_FD(X, 6) BNPP_CHAIN_SPLIT_FD(X, 7) \
+    BNPP_CHAIN_SPLIT_FD(X, 8)
+
+}  // namespace bnpp

@@ -134,12 +134,18 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         if (cards[b.chain_x[j]] != K || (!sum && cards[b.chain_n[j]] != K)) return fail("chain: mixed cardinalities");
         N *= K;
     }
-    if (N > 64 || (K != 2 && K != 4)) return fail("chain: register table too large");
+    // split form (chainsplit.cuh): binary fp32 runs of 5..8 buckets over 2^(F-4) waves
+    const char *nsp = std::getenv("BNPP_NO_SPLIT");
+    const char *smf = std::getenv("BNPP_SPLIT_MIN_F");
+    const int split_min = smf ? std::max(5, std::atoi(smf)) : 5;
+    const bool split_ok = !(nsp && *nsp == '1') && K == 2 && eb == 4 && F >= split_min && F <= 8;
+    if ((N > 64 && !split_ok) || (K != 2 && K != 4)) return fail("chain: register table too large");
     std::vector<int> gidx(F, -1);                     // input index of G_j (-1: absent)
     int ni = 1;
     for (int j = 0; j < F; ++j)
         if ((b.chain_gmask >> j) & 1) gidx[j] = ni++;
-    if (ni != (int)b.in.size() || ni > kMaxIn) return fail("chain: G tables do not match the mask");
+    if (ni != (int)b.in.size() || ni > kMaxDescIn) return fail("chain: G tables do not match the mask");
+    if (ni > kMaxIn && !split_ok) return fail("chain: more than 8 inputs need the split form");
     auto stride_of = [](const View &v, int var) -> int64_t {
         for (size_t i = 0; i < v.vars.size(); ++i)
             if (v.vars[i] == var) return v.strides[i];
@@ -226,7 +232,21 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         for (const RDim &r : md) fwd_v = fwd_v && (r.in % fv == 0 || &r == &md[0]);
         for (int p = 0; fwd_v && p < F; ++p) fwd_v = is[p] % fv == 0;
         for (int j = 0; fwd_v && j < F; ++j) fwd_v = md[0].g[j] == 0;
-        if (fwd) form = kChainFwd;
+        // split forms: 64 consecutive rest entries per workgroup along rest dim 0;
+        // forward rows contiguous (2^F entries, slot 0 slowest), backward rows
+        // read by 16-B loads (slot 0 fastest), slab stores along rest dim 0
+        bool fwd_s = split_ok && !md.empty() && md[0].card % (uint64_t)kSplitRowsHost == 0 && md[0].out == N;
+        for (int p = 0; fwd_s && p < F; ++p) fwd_s = os[p] == ((int64_t)1 << (F - 1 - p));
+        bool bwd_s = split_ok && !md.empty() && md[0].card % (uint64_t)kSplitRowsHost == 0 && md[0].out == 1 &&
+                     big.base % 4 == 0;
+        for (int p = 0; bwd_s && p < F; ++p) bwd_s = is[p] == ((int64_t)1 << p);
+        for (const RDim &r : md) bwd_s = bwd_s && r.in % 4 == 0;
+        // every bucket of a split run has its G table (no summing-only steps)
+        if (b.chain_gmask != (1 << F) - 1) fwd_s = bwd_s = false;
+        if (fwd_s) form = kChainFwdS;
+        else if (bwd_s) form = kChainBwdS;
+        else if (N > 64) return fail("chain: split form does not fit the layout");
+        else if (fwd) form = kChainFwd;
         else if (bwd) { form = kChainBwd; V = bv; }
         else return fail("chain: layout fits no kernel form");
     }
@@ -245,6 +265,11 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
             }
         }
         dep = next ? kDepNext : prev ? kDepPrev : kDepAny;
+    }
+    if (chain_split_form(form) && dep == kDepAny) {
+        if (N > 64) return fail("chain: split form needs G_j to depend on one neighbouring slot");
+        form = form == kChainFwdS ? kChainFwd : kChainBwd;             // the one-thread form, as before
+        if (form == kChainBwd) V = chain_bwd_v(N, eb);
     }
     if (fwd_v && !std::getenv("BNPP_NO_CHAIN_FWDV") && chain_supported(eb, chain_key(kChainFwdV, K, F, dep))) {
         form = kChainFwdV;
@@ -269,7 +294,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         // the streamed side linear in the thread index: a wave spans 64 * V
         // consecutive rest entries -> uniform base + 32-bit lane byte offset
         bool lin = !md.empty();
-        const bool fwdf = form == kChainFwd || form == kChainFwdV || form == kChainSum;
+        const bool fwdf = form == kChainFwd || form == kChainFwdV || form == kChainSum || form == kChainFwdS;
         int64_t s0 = md.empty() ? 0 : (fwdf ? md[0].in : md[0].out);
         for (size_t q = 0; lin && q + 1 < md.size(); ++q) {
             const int64_t a = fwdf ? md[q].in : md[q].out, nb = fwdf ? md[q + 1].in : md[q + 1].out;
@@ -279,7 +304,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         else return fail("chain: streamed side not linear in the thread index");
     }
     int32_t lo = 0;
-    for (int i = 0; i < kMaxIn; ++i) {
+    for (int i = 0; i < kMaxDescIn; ++i) {
         d.in_table[i] = i < ni ? b.in[i].table : 0;
         d.in_base[i] = i < ni ? b.in[i].base : 0;
         if (i >= 1 && i < ni) {
@@ -617,7 +642,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
 }
 
 // ---------------------------------------------------------------- VE plan
-constexpr int kChainRunMax = 6;                   // longest fused run tried (fp32, K = 2, backward)
+constexpr int kChainRunMax = 8;                   // longest fused run tried (split form: binary fp32)
 // BNPP_CHAIN_RUN_MAX (tests): a shorter cap, to exercise the short-run kernels
 inline int chain_run_max() {
     const char *e = std::getenv("BNPP_CHAIN_RUN_MAX");
@@ -1606,7 +1631,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
             d.dim_off = (int64_t)s.pool.size();
             s.pool.insert(s.pool.end(), it.pool.begin(), it.pool.end());
             d.vblk_begin = vb;
-            vb += (d.n_tiles + kBlock - 1) / kBlock;
+            const int64_t per_vb = d.chain && chain_split_form((d.chain >> 16) & 0xf) ? kSplitRowsHost : kBlock;
+            vb += (d.n_tiles + per_vb - 1) / per_vb;
             g.small_elems = std::max(g.small_elems, d.big >= 0 || d.chain ? d.small_elems : 0);
             if (dump) {
                 std::fprintf(stderr, "L%d n_in=%d k=%d tile=%dx%d big=%d bcls=%d tiles=%lld dims:", g.level, d.n_in, d.k,

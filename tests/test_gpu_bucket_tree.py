@@ -290,3 +290,39 @@ def test_short_forward_runs_vector_form(ctx, spec):
                 del os.environ[key]
     for out in res[1:]:
         assert out == res[0]
+
+
+@pytest.mark.parametrize("spec", [(16, 6, None), (18, 5, {3: 1, 40: 0}), (17, 4, None), (20, 3, {7: 0})])
+def test_split_runs_identical_to_unfused(ctx, capfd, spec):
+    """Binary fp32 sweeps tall enough for the split chain form (chainsplit.cuh:
+    runs of 5..8 buckets, the 2^F table of a rest entry over 2^(F-4) waves):
+    partition and tree marginals bit-identical to the one-thread runs of <= 6
+    buckets and to one bucket per launch; the plan holds split runs (forms 5, 6)."""
+    r, c, ev = spec
+    ev = ev or {}
+    m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=13))
+    col = [i * c + j for j in range(c) for i in range(r)]
+    knobs = [{"BNPP_DEBUG_CHAIN": "1"}, {"BNPP_SPLIT_MIN_F": "7"}, {"BNPP_NO_SPLIT": "1"},
+             {"BNPP_NO_SPLIT": "1", "BNPP_CHAIN_RUN_MAX": "6"}, {"BNPP_NO_CHAIN": "1"}]
+    res = []
+    for kn in knobs:
+        os.environ.update(kn)
+        os.environ["BNPP_TREE_SLOTS"] = "3"
+        capfd.readouterr()
+        try:
+            # evidence in the partition only (it can branch the bucket tree, and
+            # BNPP_TREE_SLOTS forces the checkpointed chain plan)
+            out = [bnpp.partition(ctx, m, ev, "mf", bnpp.F32, order=col)[0],
+                   bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F32, order=col)[0]]
+            res.append(out)
+        finally:
+            for key in list(kn) + ["BNPP_TREE_SLOTS"]:
+                del os.environ[key]
+        if "BNPP_DEBUG_CHAIN" in kn:
+            err = capfd.readouterr().err
+            assert "run form 5 K=2 F=8" in err or "run form 6 K=2 F=8" in err, err[-2000:]
+    for out in res[1:]:
+        assert out == res[0]
+    want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    for t in range(m.n_vars):
+        assert _close(res[0][1][t], want[t], 1e-5), (t, res[0][1][t], want[t])

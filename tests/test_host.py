@@ -269,12 +269,18 @@ def test_plan_short_forward_runs_use_vector_form(capfd):
 
 def test_plan_forward_runs_of_six(capfd):
     """Binary fp32 sweeps of a checkpointed bucket tree fuse 6 forward buckets
-    per pass (256-B rows staged in 128-B parts) and 6 backward ones."""
+    per pass (256-B rows staged in 128-B parts) and 6 backward ones in the
+    one-thread forms; with the split forms (chainsplit.cuh) runs of 7-8."""
     from bnpp import synth
     m = bnpp.Model.from_dict(synth.ising_grid(16, 5, seed=11))
     col = [i * 5 + j for j in range(5) for i in range(16)]
-    forms = _chain_forms(capfd, m, col, {"BNPP_TREE_SLOTS": "3"}, kind=3)
+    forms = _chain_forms(capfd, m, col, {"BNPP_TREE_SLOTS": "3", "BNPP_NO_SPLIT": "1"}, kind=3)
     assert (1, 6) in forms and (2, 6) in forms, forms
+    m = bnpp.Model.from_dict(synth.ising_grid(18, 5, seed=11))
+    col = [i * 5 + j for j in range(5) for i in range(18)]
+    forms = _chain_forms(capfd, m, col, {"BNPP_TREE_SLOTS": "3"}, kind=3)
+    assert (5, 8) in forms and (6, 8) in forms, forms
+    assert max(f for _, f in forms) == 8
 
 
 def test_checkpoint_slot_memo_matches_fresh_search():

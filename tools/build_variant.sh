@@ -7,11 +7,12 @@ cd "$(dirname "$0")/../bn-pp_amd"
 name=$1; flags=$2
 make -s -j8 lib/libbnpp.so
 mkdir -p build_$name lib_$name
-for f in launch k_generic_f32 k_generic_f64 k_stream_f32 k_stream_f64 k_chain_f32 k_chain_f64; do
+for src in csrc/*.hip; do
+  f=$(basename $src .hip)
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Icsrc -I../include $flags \
-      -c csrc/$f.hip -o build_$name/$f.o &
+      -c $src -o build_$name/$f.o &
 done
 wait
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib_$name/libbnpp.so build_$name/*.o \
-    build/bp.o build/plan.o build/order.o build/model_io.o build/runtime.o build/capi.o build/bn_api.o -Wl,-soname,libbnpp.so -pthread
+    build/plan.o build/order.o build/model_io.o build/runtime.o build/capi.o build/bn_api.o -Wl,-soname,libbnpp.so -pthread
 echo "built lib_$name"
