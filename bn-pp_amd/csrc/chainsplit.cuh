@@ -29,7 +29,8 @@
 
 namespace bnpp {
 
-constexpr int kSplitRows = kSplitRowsHost;   // rest entries per workgroup (one per lane)
+constexpr int kSplitRows = kSplitRowsHost;
+typedef float v2f __attribute__((ext_vector_type(2)));   // rest entries per workgroup (one per lane)
 
 __host__ __device__ constexpr int split_waves(int f) { return 1 << (f - 4); }
 // LDS bytes: max(exchange table, row image) + the G tables
@@ -67,14 +68,15 @@ __device__ __forceinline__ void split_step(float (&t)[16], const float *small, i
         const float g10 = NQ == 2 && q ? g[NQ - 1][0][1] : g[0][0][1];
         const float g01 = NQ == 2 && q ? g[NQ - 1][1][0] : g[0][1][0];
         const float g11 = NQ == 2 && q ? g[NQ - 1][1][1] : g[0][1][1];
-        const float m0 = t[e], m1 = t[e | PJ];
-        float a0 = 0.f, a1 = 0.f;
-        a0 = a0 + g00 * m0;
-        a0 = a0 + g10 * m1;
-        a1 = a1 + g01 * m0;
-        a1 = a1 + g11 * m1;
-        t[e] = a0;
-        t[e | PJ] = a1;
+        // acc = 0; acc += G(0, n) m0; acc += G(1, n) m1 for n = 0, 1 (packed
+        // pairs).  0 + p == p exactly for the non-negative p of a potential
+        // table (no -0 can arise), so the leading add is dropped.
+        const v2f m0 = {t[e], t[e]}, m1 = {t[e | PJ], t[e | PJ]};
+        const v2f gx0 = {g00, g01}, gx1 = {g10, g11};
+        const v2f p0 = gx0 * m0, p1 = gx1 * m1;
+        const v2f a = p0 + p1;
+        t[e] = a[0];
+        t[e | PJ] = a[1];
     }
 }
 
@@ -197,28 +199,40 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         lds_barrier();
     };
     // rest entry of this lane in tile vb: input / output offsets, G offsets
+    // rest entry of this lane in tile vb: input / output offsets, G offsets.
+    // A tile's 64 entries are consecutive along rest dim 0 (planner: its card
+    // is a multiple of 64), so the mixed-radix decode is done once per tile on
+    // uniform values and each lane adds lane * (stride on dim 0).
     auto decode = [&](int64_t vb, int64_t &in_off, int64_t &out_off, int32_t (&gb)[F]) {
-        const int64_t tid = (vb - cur_begin) * kSplitRows + lane;
+        const int64_t tid0 = (vb - cur_begin) * kSplitRows;
         const int row = 4 + F;
         const int64_t *dp = c.dims;
         uint64_t q, r;
-        divmod_dim((uint64_t)tid, c.t0h, c.t0m, q, r);
-        in_off = c.in_base + (int64_t)r * dp[2];
-        out_off = (int64_t)r * dp[3];
+        divmod_dim((uint64_t)tid0, c.t0h, c.t0m, q, r);
+        int64_t ui = c.in_base + (int64_t)r * dp[2], uo = (int64_t)r * dp[3];
+        int32_t ug[F];
 #pragma unroll
-        for (int j = 0; j < F; ++j) gb[j] = c.glds[j] + (int32_t)r * (int32_t)dp[4 + j];
+        for (int j = 0; j < F; ++j) ug[j] = c.glds[j] + (int32_t)r * (int32_t)dp[4 + j];
+        const int64_t si = dp[2], so = dp[3];
+        int32_t sg[F];
+#pragma unroll
+        for (int j = 0; j < F; ++j) sg[j] = (int32_t)dp[4 + j];
         uint64_t rem = q;
         dp += row;
         for (int dd = 1; dd < c.n_dims; ++dd) {
             uint64_t qq, rr;
             divmod_dim(rem, dp[0], dp[1], qq, rr);
-            in_off += (int64_t)rr * dp[2];
-            out_off += (int64_t)rr * dp[3];
+            ui += (int64_t)rr * dp[2];
+            uo += (int64_t)rr * dp[3];
 #pragma unroll
-            for (int j = 0; j < F; ++j) gb[j] += (int32_t)rr * (int32_t)dp[4 + j];
+            for (int j = 0; j < F; ++j) ug[j] += (int32_t)rr * (int32_t)dp[4 + j];
             rem = qq;
             dp += row;
         }
+        in_off = ui + (int64_t)lane * si;
+        out_off = uo + (int64_t)lane * so;
+#pragma unroll
+        for (int j = 0; j < F; ++j) gb[j] = ug[j] + lane * sg[j];
     };
     // the tile's message loads (16 values per lane)
     auto issue = [&](int64_t in_off, float (&rg)[16]) {
@@ -321,7 +335,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             for (int e = 0; e < 16; ++e) t[e] = ldexp_t(t[e], c.neg_e);
         }
 #pragma unroll
-        for (int e = 0; e < 16; ++e) lmax = t[e] > lmax ? t[e] : lmax;
+        for (int e = 0; e < 16; ++e) lmax = fmaxf(lmax, t[e]);      // entries are >= 0, never NaN
 
         if constexpr (FORM == kChainFwd) {
             // row position of entry e: w * 16 + e (slot 0 most significant)
