@@ -29,15 +29,14 @@
 
 namespace bnpp {
 
-constexpr int kSplitRows = kSplitRowsHost;
-typedef float v2f __attribute__((ext_vector_type(2)));   // rest entries per workgroup (one per lane)
+constexpr int kSplitRows = kSplitRowsHost;   // rest entries per workgroup (one per lane)
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 __host__ __device__ constexpr int split_waves(int f) { return 1 << (f - 4); }
-// LDS bytes: max(exchange table, row image) + the G tables
-__host__ __device__ constexpr int split_img_bytes(int f) {
-    return kSplitRows * ((1 << f) * 4 + 16) > kSplitRows * (1 << f) * 4 ? kSplitRows * ((1 << f) * 4 + 16)
-                                                                         : kSplitRows * (1 << f) * 4;
-}
+// LDS bytes: the exchange table and the row image, side by side (so a tile
+// needs two barriers, not four), then the G tables
+__host__ __device__ constexpr int split_xch_bytes(int f) { return kSplitRows * (1 << f) * 4; }
+__host__ __device__ constexpr int split_img_bytes(int f) { return kSplitRows * ((1 << f) * 4 + 16); }
 
 // One bucket J (slot J, 0-3 in phase 1, 4..F-1 in phase 2) on the lane's 16
 // entries.  The local index e holds the local slots' digits; digit(e, p) gives
@@ -143,6 +142,12 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
     c.neg_e = (int)(-e_sum);
 }
 
+#ifndef BNPP_SPLIT_FLAT
+#define BNPP_SPLIT_FLAT 0     // 1: one tile per workgroup (flat grid), no prefetch
+#endif
+#ifndef BNPP_SPLIT_NTL
+#define BNPP_SPLIT_NTL 0      // nontemporal message loads
+#endif
 #ifndef BNPP_SPLIT_WAVES
 #define BNPP_SPLIT_WAVES 0     // waves per SIMD the register allocation must allow (0: compiler's choice)
 #endif
@@ -168,9 +173,9 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     constexpr int CPR = N / 4;                             // backward: 16-B chunks per row
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
-    unsigned char *img = dyn + kRedBytes;
-    T *xch = reinterpret_cast<T *>(img);
-    T *small = reinterpret_cast<T *>(dyn + kRedBytes + split_img_bytes(F));
+    T *xch = reinterpret_cast<T *>(dyn + kRedBytes);
+    unsigned char *img = dyn + kRedBytes + split_xch_bytes(F);
+    T *small = reinterpret_cast<T *>(dyn + kRedBytes + split_xch_bytes(F) + split_img_bytes(F));
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // digit of slot p (4 <= p < F) in phase 1: bit (F-1-p) of w
     auto wdig = [&](int p) { return (w >> (F - 1 - p)) & 1; };
@@ -247,7 +252,9 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
 #pragma unroll
                 for (int p = 0; p < 4; ++p) o += (int64_t)((e >> (3 - p)) & 1) * c.is4[p];
                 const T *sp = wb + o;                      // uniform slab base
-                rg[e] = gload(reinterpret_cast<const T *>(reinterpret_cast<const char *>(sp) + lob));
+                const T *src = reinterpret_cast<const T *>(reinterpret_cast<const char *>(sp) + lob);
+                if constexpr (BNPP_SPLIT_NTL != 0) rg[e] = __builtin_nontemporal_load((const gbl_t<T> *)src);
+                else rg[e] = gload(src);
             }
         } else {
             // 64 input rows of N contiguous values (slot 0 fastest): wave w loads
@@ -258,7 +265,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 const int q = it * 64 + lane;
                 const int rw = w * RPW + q / CPR, ch = q % CPR;
                 const int64_t ro = __shfl(in_off, rw, 64);  // row rw's input offset (held by lane rw)
-                const vec_t<T, 4> v = vload<4, kNtLoad, true>(big + ro + 4 * ch);
+                const vec_t<T, 4> v = vload<4, kNtLoad || BNPP_SPLIT_NTL != 0, true>(big + ro + 4 * ch);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) rg[4 * it + k] = v[k];
             }
@@ -281,8 +288,10 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     };
 
     // one tile: the 16 values per lane in t, this lane's rest entry decoded
+    // Barriers per tile: forward  [phase 1, xch write] B [xch read, phase 2, image write] B [image read];
+    // backward [image write] B [image read, phase 1, xch write] B [xch read, phase 2].  A wave past one
+    // of them knows every wave has finished the previous tile's reads of the region it writes next.
     auto run_tile = [&](float (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
-        lds_barrier();                                     // the previous tile's LDS reads are done
         if constexpr (FORM == kChainBwd) {
             // rows through the image, then this lane's 16 entries (slots 4.. = w)
 #pragma unroll
@@ -302,7 +311,6 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 const int pos = fixed + (((e >> 3) & 1) | (((e >> 2) & 1) << 1) | (((e >> 1) & 1) << 2) | ((e & 1) << 3));
                 t[e] = *reinterpret_cast<const T *>(img + lane * ROWB + 4 * pos);
             }
-            lds_barrier();                                 // the image (aliased by the exchange) has been read
         }
 
         // phase 1: buckets 0-3 (other slots: local bits of e, slots >= 4 from w)
@@ -339,7 +347,6 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
 
         if constexpr (FORM == kChainFwd) {
             // row position of entry e: w * 16 + e (slot 0 most significant)
-            lds_barrier();                                 // every wave has read the exchange table
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4)
                 *reinterpret_cast<vec_t<T, 4> *>(img + lane * ROWB + 4 * (w * 16 + 4 * c4)) =
@@ -380,7 +387,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     float rg[16];
     int64_t in_off, out_off;
     int32_t gb[F];
-    if (n_desc == 1) {
+    if (n_desc == 1 && BNPP_SPLIT_FLAT == 0) {
         // one bucket: the next tile's loads are issued (unconditionally: the
         // last tile is re-read rather than branching, so the wait counts stay
         // static) before the current tile is computed
@@ -421,7 +428,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
 #endif
 template <int F, int FORM, int DEP>
 static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_t stream) {
-    const size_t shm = kRedBytes + split_img_bytes(F) + (size_t)small_elems * sizeof(float);
+    const size_t shm = kRedBytes + split_xch_bytes(F) + split_img_bytes(F) + (size_t)small_elems * sizeof(float);
     static const hipError_t attr = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (attr != hipSuccess) return attr;
@@ -433,7 +440,7 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
             cus = 256;
     }
     const int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
-    const int64_t grid = a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
+    const int64_t grid = BNPP_SPLIT_FLAT ? a.vblocks : a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
     hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP>), dim3((unsigned)grid), dim3(64 * split_waves(F)), shm,
                        stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
     return hipGetLastError();

@@ -1645,7 +1645,9 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 }
                 std::fprintf(stderr, " es:");
                 for (int q = 0; q < d.n_in; ++q) std::fprintf(stderr, "%s%lld", q ? "," : "", (long long)d.elim_stride[q]);
-                std::fprintf(stderr, "\n");
+                std::fprintf(stderr, " tables:");
+                for (int q = 0; q < d.n_in; ++q) std::fprintf(stderr, "%s%d", q ? "," : "", d.in_table[q]);
+                std::fprintf(stderr, "->%d\n", d.out_table);
             }
             s.descs.push_back(d);
         }
