@@ -387,10 +387,11 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     float rg[16];
     int64_t in_off, out_off;
     int32_t gb[F];
-    if (n_desc == 1 && BNPP_SPLIT_FLAT == 0) {
-        // one bucket: the next tile's loads are issued (unconditionally: the
-        // last tile is re-read rather than branching, so the wait counts stay
-        // static) before the current tile is computed
+    if (n_desc == 1 && BNPP_SPLIT_FLAT == 0 && FORM == kChainBwd) {
+        // one bucket, backward form: the next tile's loads are issued
+        // (unconditionally: the last tile is re-read rather than branching, so
+        // the wait counts stay static) before the current tile is computed; a
+        // second register set spills here (the row loads' addresses are live)
         decode(vb, in_off, out_off, gb);
         issue(in_off, rg);
         while (true) {
@@ -403,6 +404,38 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             decode(vb, in_off, out_off, gb);
             run_tile(t, out_off, gb);
             vb = vbn;
+            if (vb >= total_vblocks) break;
+        }
+    } else if (n_desc == 1 && BNPP_SPLIT_FLAT == 0) {
+        // one bucket, forward form: the loads of the next two tiles are in flight while a
+        // tile is computed (register sets A and B alternate: a set is copied
+        // out only once its loads are two tiles old, so no wait exposes
+        // fresh-load latency); loads are issued unconditionally (the last
+        // tile is re-read rather than branching) so the wait counts stay static
+        const int64_t last = total_vblocks - 1, g = gridDim.x;
+        auto clamp = [&](int64_t v) { return v < last ? v : last; };
+        float rb[16];
+        decode(vb, in_off, out_off, gb);
+        issue(in_off, rg);
+        decode(clamp(vb + g), in_off, out_off, gb);
+        issue(in_off, rb);
+        while (true) {
+            float t[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) t[e] = rg[e];
+            decode(clamp(vb + 2 * g), in_off, out_off, gb);
+            issue(in_off, rg);
+            decode(vb, in_off, out_off, gb);
+            run_tile(t, out_off, gb);
+            vb += g;
+            if (vb >= total_vblocks) break;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) t[e] = rb[e];
+            decode(clamp(vb + 2 * g), in_off, out_off, gb);
+            issue(in_off, rb);
+            decode(vb, in_off, out_off, gb);
+            run_tile(t, out_off, gb);
+            vb += g;
             if (vb >= total_vblocks) break;
         }
     } else {
