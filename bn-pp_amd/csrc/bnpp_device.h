@@ -22,6 +22,14 @@ namespace bnpp {
 constexpr int kMaxIn = 8;          // inputs per fused launch; longer chains are split
 constexpr int kMaxDescIn = 9;      // descriptor slots: a fused run of 8 buckets has 8 G tables + the message
 constexpr int kSplitRowsHost = 64; // rest entries per workgroup of the split chain forms (chainsplit.cuh)
+// split forms: each G_j staged in LDS packed, 8 entries [q][n][x] per base
+// offset (one 32-B pair of 16-B reads per bucket); LDS per workgroup: the
+// reduction scratch, the exchange table, the row image, then the packed G
+constexpr int kSplitPack = 8;
+constexpr int kSplitLdsBytes = 160 * 1024;
+constexpr int split_xch_bytes(int f) { return kSplitRowsHost * (1 << f) * 4; }
+constexpr int split_img_bytes(int f) { return kSplitRowsHost * ((1 << f) * 4 + 16); }
+constexpr int split_g_budget_bytes(int f) { return kSplitLdsBytes - 64 - split_xch_bytes(f) - split_img_bytes(f); }
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 
 // One per table (source factor or message), resident in device memory.

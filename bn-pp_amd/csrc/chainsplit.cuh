@@ -31,33 +31,34 @@ namespace bnpp {
 
 constexpr int kSplitRows = kSplitRowsHost;   // rest entries per workgroup (one per lane)
 typedef float v2f __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+static_assert(kRedBytes == 64, "split_g_budget_bytes assumes 64 B of reduction scratch");
 
 __host__ __device__ constexpr int split_waves(int f) { return 1 << (f - 4); }
-// LDS bytes: the exchange table and the row image, side by side (so a tile
-// needs two barriers, not four), then the G tables
-__host__ __device__ constexpr int split_xch_bytes(int f) { return kSplitRows * (1 << f) * 4; }
-__host__ __device__ constexpr int split_img_bytes(int f) { return kSplitRows * ((1 << f) * 4 + 16); }
+// LDS: the exchange table and the row image side by side (so a tile needs two
+// barriers, not four), then the packed G tables (split_xch_bytes /
+// split_img_bytes / kSplitPack, bnpp_device.h)
 
 // One bucket J (slot J, 0-3 in phase 1, 4..F-1 in phase 2) on the lane's 16
 // entries.  The local index e holds the local slots' digits; digit(e, p) gives
 // any slot's digit for entry e (local ones from e, the others wave-uniform).
 template <int F, int PH, int J, int DEP, typename Digit>
-__device__ __forceinline__ void split_step(float (&t)[16], const float *small, int32_t gb, int32_t gsj, int32_t gsq,
-                                           int32_t gsn, Digit &&digit) {
+__device__ __forceinline__ void split_step(float (&t)[16], const float *gp, Digit &&digit) {
     // place of slot J in the local index
     constexpr int PJ = PH == 1 ? (8 >> J) : (1 << (F - 1 - J));
     constexpr int Q = DEP == kDepNext ? J + 1 : J - 1;
     constexpr bool HASQ = Q >= 0 && Q < F;
-    // the bucket's G values, fetched once: [q][n][x] (q: digit of slot Q)
+    // the bucket's G values, fetched once from the packed table: [q][n][x]
+    // (q: digit of slot Q), one 16-B read per q
     constexpr int NQ = HASQ ? 2 : 1;
     float g[NQ][2][2];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const int32_t go = gb + (HASQ ? q * gsq : 0);
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int x = 0; x < 2; ++x) g[q][n][x] = small[go + x * gsj + n * gsn];
+        const v4f v = *reinterpret_cast<const v4f *>(gp + 4 * q);
+        g[q][0][0] = v[0];
+        g[q][0][1] = v[1];
+        g[q][1][0] = v[2];
+        g[q][1][1] = v[3];
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -195,16 +196,22 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         split_load_state<F, DEP>(c, d, pool + d.dim_off, meta, w);
         if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta);
         lds_barrier();                                     // the previous bucket's tables are no longer read
-        for (int i = 1; i < kMaxDescIn; ++i) {
-            if (i >= d.n_in) break;
-            const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
-            const int off = d.in_lds_off[i], span = d.in_span[i];
-            for (int e = threadIdx.x; e < span; e += 64 * W) small[off + e] = gload(src + e);
+        // G_j packed: entry (o, q, n, x) at 8 o + 4 q + 2 n + x holds G_j[o + q
+        // gsq + n gsn + x gsj] (gmask is all ones: G_j is input j + 1)
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+            const T *src = static_cast<const T *>(meta[d.in_table[j + 1]].ptr) + d.in_base[j + 1];
+            const int span = d.in_span[j + 1];
+            T *dst = small + d.in_lds_off[j + 1];
+            for (int e = threadIdx.x; e < span * kSplitPack; e += 64 * W) {
+                const int si = (e >> 3) + ((e >> 2) & 1) * c.gsq[j] + ((e >> 1) & 1) * c.gsn[j] + (e & 1) * c.gsj[j];
+                dst[e] = si < span ? gload(src + si) : T(0);
+            }
         }
         lds_barrier();
     };
     // rest entry of this lane in tile vb: input / output offsets, G offsets
-    // rest entry of this lane in tile vb: input / output offsets, G offsets.
+    // (base offsets into the native G tables; packed entries at kSplitPack x).
     // A tile's 64 entries are consecutive along rest dim 0 (planner: its card
     // is a multiple of 64), so the mixed-radix decode is done once per tile on
     // uniform values and each lane adds lane * (stride on dim 0).
@@ -217,7 +224,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         int64_t ui = c.in_base + (int64_t)r * dp[2], uo = (int64_t)r * dp[3];
         int32_t ug[F];
 #pragma unroll
-        for (int j = 0; j < F; ++j) ug[j] = c.glds[j] + (int32_t)r * (int32_t)dp[4 + j];
+        for (int j = 0; j < F; ++j) ug[j] = (int32_t)r * (int32_t)dp[4 + j];
         const int64_t si = dp[2], so = dp[3];
         int32_t sg[F];
 #pragma unroll
@@ -317,7 +324,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         auto dig1 = [&](int e, int p) { return p < 4 ? (e >> (3 - p)) & 1 : wdig(p); };
         static_for<4>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            split_step<F, 1, j, DEP>(t, small, gb[j], c.gsj[j], c.gsq[j], c.gsn[j], dig1);
+            split_step<F, 1, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig1);
         });
         // exchange: entry (n-digits 0-3 = e, slots 4.. = w) -> xch[(w * 16 + e) * 64 + lane]
 #pragma unroll
@@ -336,7 +343,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         };
         static_for<F - 4>([&](auto jc) {
             constexpr int j = 4 + decltype(jc)::value;
-            split_step<F, 2, j, DEP>(t, small, gb[j], c.gsj[j], c.gsq[j], c.gsn[j], dig2);
+            split_step<F, 2, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig2);
         });
         if (c.flags & kScale) {
 #pragma unroll

@@ -266,8 +266,17 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         }
         dep = next ? kDepNext : prev ? kDepPrev : kDepAny;
     }
-    if (chain_split_form(form) && dep == kDepAny) {
-        if (N > 64) return fail("chain: split form needs G_j to depend on one neighbouring slot");
+    // split forms stage G_j packed (kSplitPack entries per base offset)
+    int64_t g_pk = 0;
+    for (int i = 1; i < ni; ++i) {
+        int64_t sp = 1;
+        for (size_t q = 0; q < b.in[i].vars.size(); ++q) sp += (int64_t)(cards[b.in[i].vars[q]] - 1) * b.in[i].strides[q];
+        g_pk += sp * kSplitPack;
+    }
+    const bool pk_fits = g_pk * 4 <= split_g_budget_bytes(F);
+    if (chain_split_form(form) && (dep == kDepAny || !pk_fits)) {
+        if (N > 64) return fail(pk_fits ? "chain: split form needs G_j to depend on one neighbouring slot"
+                                        : "chain: packed G tables exceed the split form's LDS");
         form = form == kChainFwdS ? kChainFwd : kChainBwd;             // the one-thread form, as before
         if (form == kChainBwd) V = chain_bwd_v(N, eb);
     }
@@ -314,11 +323,12 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
             if (sp > kStreamSmallMax) return fail("chain: G table too large for LDS");
             d.in_span[i] = (int32_t)sp;
             d.in_lds_off[i] = lo;
-            lo += (int32_t)((sp + 3) & ~3);
+            lo += chain_split_form(form) ? (int32_t)(sp * kSplitPack) : (int32_t)((sp + 3) & ~3);
         }
     }
     d.small_elems = lo;
-    if ((int64_t)lo * eb > kStreamLdsBudget) return fail("chain: G tables exceed the LDS budget");
+    if ((int64_t)lo * eb > (chain_split_form(form) ? split_g_budget_bytes(F) : kStreamLdsBudget))
+        return fail("chain: G tables exceed the LDS budget");
     {
         uint32_t shift, magic;
         bool pow2;
