@@ -326,3 +326,25 @@ def test_split_runs_identical_to_unfused(ctx, capfd, spec):
     want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
     for t in range(m.n_vars):
         assert _close(res[0][1][t], want[t], 1e-5), (t, res[0][1][t], want[t])
+
+
+@pytest.mark.parametrize("keep,slow", [(3, 13), (5, 13), (7, 2), (9, 4)])
+def test_tree_chain_kept_sets_match(ctx, keep, slow):
+    """Deliveries from kept sets smaller than the separators (the 32x32 path:
+    slow variables summed in one composite pass, the others reduced from the
+    kept table; targets never kept get their own reduction), forced on a
+    12x10 column sweep by shrinking the kept / slow limits: same marginals as
+    the per-target engine."""
+    m = bnpp.Model.from_dict(synth.ising_grid(12, 10, seed=12))
+    col = [r * 10 + c for c in range(10) for r in range(12)]
+    want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    os.environ.update({"BNPP_KEEP_LOG2": str(keep), "BNPP_SLOW_LOG2": str(slow), "BNPP_TREE_SLOTS": "3"})
+    try:
+        got, _ = bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64, order=col)
+        got32, _ = bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F32, order=col)
+    finally:
+        for k in ("BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_TREE_SLOTS"):
+            os.environ.pop(k, None)
+    for t in range(m.n_vars):
+        assert _close(got[t], want[t], 1e-12), (keep, slow, t, got[t], want[t])
+        assert _close(got32[t], want[t], 1e-5), (keep, slow, t, got32[t], want[t])
