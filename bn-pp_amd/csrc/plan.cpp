@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <set>
 #include <thread>
 #include <climits>
 #include <cmath>
@@ -1460,19 +1461,28 @@ int64_t plan_peak_bytes(const VEPlan &p, int elem_bytes) {
 // ------------------------------------------------------------- schedule
 namespace {
 struct Arena {
-    std::map<int64_t, int64_t> free_;   // offset -> length
+    // free blocks indexed by offset (merging) and by (length, offset) (best fit)
+    std::map<int64_t, int64_t> free_;            // offset -> length
+    std::set<std::pair<int64_t, int64_t>> by_len_;   // (length, offset)
     int64_t top = 0;
+    void add_free(int64_t off, int64_t len) {
+        free_[off] = len;
+        by_len_.insert({len, off});
+    }
+    void erase_free(std::map<int64_t, int64_t>::iterator it) {
+        by_len_.erase({it->second, it->first});
+        free_.erase(it);
+    }
     int64_t alloc(int64_t n) {
         n = (n + 255) & ~(int64_t)255;
-        // best fit: the smallest free block that holds n (small temporaries go
-        // into small holes instead of splitting the holes big messages need)
-        auto best = free_.end();
-        for (auto it = free_.begin(); it != free_.end(); ++it)
-            if (it->second >= n && (best == free_.end() || it->second < best->second)) best = it;
-        if (best != free_.end()) {
-            int64_t off = best->first, len = best->second;
-            free_.erase(best);
-            if (len > n) free_[off + n] = len - n;
+        // best fit: the smallest free block that holds n, lowest offset among
+        // equals (small temporaries go into small holes instead of splitting
+        // the holes big messages need); O(log blocks)
+        auto b = by_len_.lower_bound({n, INT64_MIN});
+        if (b != by_len_.end()) {
+            const int64_t off = b->second, len = b->first;
+            erase_free(free_.find(off));
+            if (len > n) add_free(off + n, len - n);
             return off;
         }
         // extend: merge with a trailing free block if present
@@ -1480,7 +1490,7 @@ struct Arena {
             auto last = std::prev(free_.end());
             if (last->first + last->second == top) {
                 int64_t off = last->first;
-                free_.erase(last);
+                erase_free(last);
                 top = off + n;
                 return off;
             }
@@ -1491,19 +1501,22 @@ struct Arena {
     }
     void release(int64_t off, int64_t n) {
         n = (n + 255) & ~(int64_t)255;
-        auto it = free_.emplace(off, n).first;
-        auto nx = std::next(it);
-        if (nx != free_.end() && it->first + it->second == nx->first) {
-            it->second += nx->second;
-            free_.erase(nx);
+        auto nx = free_.lower_bound(off);
+        if (nx != free_.end() && off + n == nx->first) {     // merge the next block
+            n += nx->second;
+            erase_free(nx);
         }
+        auto it = free_.lower_bound(off);
         if (it != free_.begin()) {
             auto pv = std::prev(it);
-            if (pv->first + pv->second == it->first) {
-                pv->second += it->second;
-                free_.erase(it);
+            if (pv->first + pv->second == off) {            // merge into the previous block
+                const int64_t po = pv->first, pl = pv->second;
+                erase_free(pv);
+                add_free(po, pl + n);
+                return;
             }
         }
+        add_free(off, n);
     }
 };
 }  // namespace
