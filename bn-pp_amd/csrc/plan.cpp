@@ -915,10 +915,29 @@ struct PlanBuilder {
     // layout, t slowest), they are summed in a few composite passes of
     // <= ~2K values each (about one read of the inputs); otherwise one
     // variable at a time in elimination-rank order.
-    int reduce_to(std::vector<View> in, int t) {
+    int reduce_to(std::vector<View> in, int t) { return reduce_keep(std::move(in), {t}); }
+    // the marginals of several targets of one table: the targets are split in
+    // two halves (by position in the table's layout), each half's joint is
+    // summed out of the table once, and the halves recurse; every big table
+    // is read twice instead of once per target
+    void reduce_many(const View &v, std::vector<int> tg, std::vector<int> &result_of) {
+        if (tg.size() <= 2 || table_size(v.vars, cards) <= 4096) {
+            for (int t : tg) result_of[t] = reduce_to({v}, t);
+            return;
+        }
+        auto pos = [&](int t) { return std::find(v.vars.begin(), v.vars.end(), t) - v.vars.begin(); };
+        std::sort(tg.begin(), tg.end(), [&](int a, int b) { return pos(a) < pos(b); });
+        const size_t h = tg.size() / 2;
+        for (int side = 0; side < 2; ++side) {
+            std::vector<int> part(side ? tg.begin() + h : tg.begin(), side ? tg.end() : tg.begin() + h);
+            reduce_many(view(reduce_keep({v}, part)), part, result_of);
+        }
+    }
+    // sum every variable outside `keep` out of the product of `in`
+    int reduce_keep(std::vector<View> in, const std::vector<int> &keep) {
         std::vector<int> y;
         for (int v : chain_scope(in))
-            if (v != t) y.push_back(v);
+            if (!contains(keep, v)) y.push_back(v);
         std::sort(y.begin(), y.end(), [&](int a, int b) { return rank[a] < rank[b]; });
         if (y.empty()) return emit(in, -1, false);
         while (!y.empty()) {
@@ -1340,8 +1359,12 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 } else {
                     tb = B.emit(bel, slow[j].empty() ? -1 : slow[j][0], false);
                 }
-                for (int t : mit->second)
-                    result_of[t] = tb >= 0 ? B.reduce_to({B.view(tb)}, t) : B.reduce_to(bel, t);
+                if (tb >= 0 && !std::getenv("BNPP_NO_REDUCE_MANY")) {
+                    B.reduce_many(B.view(tb), mit->second, result_of);
+                } else {
+                    for (int t : mit->second)
+                        result_of[t] = tb >= 0 ? B.reduce_to({B.view(tb)}, t) : B.reduce_to(bel, t);
+                }
             }
             auto dit = direct.find(j);
             if (dit != direct.end())
