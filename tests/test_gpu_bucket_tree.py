@@ -348,3 +348,34 @@ def test_tree_chain_kept_sets_match(ctx, keep, slow):
     for t in range(m.n_vars):
         assert _close(got[t], want[t], 1e-12), (keep, slow, t, got[t], want[t])
         assert _close(got32[t], want[t], 1e-5), (keep, slow, t, got32[t], want[t])
+
+
+def test_split_runs_of_two_components_share_launches(ctx, capfd):
+    """Two disconnected 18x5 grids: their sweeps' split runs land on the same
+    levels, so a launch carries several run descriptors (the kernel's
+    multi-bucket path: per-tile bucket lookup, G tables restaged at bucket
+    changes).  log10 Z bit-identical to one-thread runs and to one bucket per
+    launch, and equal to the sum of the components' log10 Z."""
+    a, b = synth.ising_grid(18, 5, seed=21), synth.ising_grid(18, 5, seed=22)
+    n = len(a["cards"])
+    md = {"type": "MARKOV", "cards": a["cards"] + b["cards"],
+          "scopes": a["scopes"] + [[v + n for v in s] for s in b["scopes"]], "values": a["values"] + b["values"]}
+    m = bnpp.Model.from_dict(md)
+    col = [i * 5 + j for j in range(5) for i in range(18)]
+    order = col + [v + n for v in col]
+    res = []
+    for kn in ({"BNPP_DUMP_PLAN": "1"}, {"BNPP_NO_SPLIT": "1"}, {"BNPP_NO_CHAIN": "1"}):
+        os.environ.update(kn)
+        capfd.readouterr()
+        try:
+            res.append(bnpp.partition(ctx, m, {}, "mf", bnpp.F32, order=order)[0])
+        finally:
+            for key in kn:
+                del os.environ[key]
+        if "BNPP_DUMP_PLAN" in kn:
+            runs = [ln.split()[0] for ln in capfd.readouterr().err.splitlines() if " n_in=9 " in ln]
+            assert runs and max(runs.count(lv) for lv in runs) >= 2, runs
+    assert res[1] == res[0] and res[2] == res[0]
+    ma, mb = bnpp.Model.from_dict(a), bnpp.Model.from_dict(b)
+    want = bnpp.partition(ctx, ma, {}, "mf", bnpp.F64, order=col)[0] + bnpp.partition(ctx, mb, {}, "mf", bnpp.F64, order=col)[0]
+    assert abs(res[0] - want) <= 1e-6 * abs(want), (res[0], want)
