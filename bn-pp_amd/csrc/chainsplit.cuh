@@ -27,9 +27,12 @@
 #pragma once
 #include "chain.cuh"
 
+#include <mutex>
+
 namespace bnpp {
 
 constexpr int kSplitRows = kSplitRowsHost;   // rest entries per workgroup (one per lane)
+constexpr int kMaxDevices = 64;
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 static_assert(kRedBytes == 64, "split_g_budget_bytes assumes 64 B of reduction scratch");
@@ -469,15 +472,30 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
 template <int F, int FORM, int DEP>
 static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_t stream) {
     const size_t shm = kRedBytes + split_xch_bytes(F) + split_img_bytes(F) + (size_t)small_elems * sizeof(float);
-    static const hipError_t attr = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (attr != hipSuccess) return attr;
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
+    // per device (a process may drive several): the 160-KiB LDS opt-in of
+    // this instantiation and the CU count the persistent grid is sized for
+    struct DevState {
+        std::mutex mu;
+        bool done[kMaxDevices] = {};
+        hipError_t attr[kMaxDevices] = {};
+        int cus[kMaxDevices] = {};
+    };
+    static DevState ds;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    int cus;
+    {
+        std::lock_guard<std::mutex> g(ds.mu);
+        if (!ds.done[dev]) {
+            ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (hipDeviceGetAttribute(&ds.cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                ds.cus[dev] <= 0)
+                ds.cus[dev] = 256;
+            ds.done[dev] = true;
+        }
+        if (ds.attr[dev] != hipSuccess) return ds.attr[dev];
+        cus = ds.cus[dev];
     }
     const int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
     const int64_t grid = BNPP_SPLIT_FLAT ? a.vblocks : a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
