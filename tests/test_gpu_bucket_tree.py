@@ -328,15 +328,16 @@ def test_split_runs_identical_to_unfused(ctx, capfd, spec):
         assert _close(res[0][1][t], want[t], 1e-5), (t, res[0][1][t], want[t])
 
 
-@pytest.mark.parametrize("keep,slow", [(3, 13), (5, 13), (7, 2), (9, 4)])
-def test_tree_chain_kept_sets_match(ctx, keep, slow):
+@pytest.mark.parametrize("keep,slow,rows", [(3, 13, 12), (5, 13, 12), (7, 2, 12), (9, 4, 12), (13, 13, 14)])
+def test_tree_chain_kept_sets_match(ctx, keep, slow, rows):
     """Deliveries from kept sets smaller than the separators (the 32x32 path:
     slow variables summed in one composite pass, the others reduced from the
     kept table; targets never kept get their own reduction), forced on a
-    12x10 column sweep by shrinking the kept / slow limits: same marginals as
-    the per-target engine."""
-    m = bnpp.Model.from_dict(synth.ising_grid(12, 10, seed=12))
-    col = [r * 10 + c for c in range(10) for r in range(12)]
+    12x10 column sweep by shrinking the kept / slow limits (14x10 with 2^13
+    kept entries: kept tables reduced hierarchically, reduce_many): same
+    marginals as the per-target engine."""
+    m = bnpp.Model.from_dict(synth.ising_grid(rows, 10, seed=12))
+    col = [r * 10 + c for c in range(10) for r in range(rows)]
     want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
     os.environ.update({"BNPP_KEEP_LOG2": str(keep), "BNPP_SLOW_LOG2": str(slow), "BNPP_TREE_SLOTS": "3"})
     try:

@@ -314,3 +314,21 @@ def test_checkpoint_slot_memo_matches_fresh_search():
                              capture_output=True, text=True, timeout=120, check=True).stdout
         assert json.loads(out.strip().splitlines()[-1]) == got
     assert here[0] == here[2] and here[0] != here[1] and here[1][1] <= budgets[1] * 1e9
+
+
+def test_plan_reduces_kept_tables_hierarchically():
+    """Deliveries with kept tables above 4096 entries reduce their targets
+    through halves (PlanBuilder::reduce_many): fewer buckets than one
+    reduction cascade per target, same traffic order of magnitude."""
+    m = bnpp.Model.from_dict(synth.ising_grid(14, 8, seed=12))
+    col = [i * 8 + j for j in range(8) for i in range(14)]
+    os.environ.update({"BNPP_KEEP_LOG2": "13", "BNPP_TREE_SLOTS": "3"})
+    try:
+        many = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+        os.environ["BNPP_NO_REDUCE_MANY"] = "1"
+        plain = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+    finally:
+        for k in ("BNPP_KEEP_LOG2", "BNPP_TREE_SLOTS", "BNPP_NO_REDUCE_MANY"):
+            os.environ.pop(k, None)
+    assert many[3] < plain[3], (many[3], plain[3])
+    assert many[6] <= plain[6] * 1.01
