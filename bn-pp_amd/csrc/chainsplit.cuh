@@ -21,9 +21,11 @@
 // contiguous, rows (2^F entries) leave through an LDS image as 4 KiB per wave.
 // Backward form (summed variables the input's fastest): the 64 input rows come
 // in by 16-B loads through the LDS image; 16 slab stores per lane.
-// Persistent grid (16 waves per CU), next tile's loads issued before the
-// current tile is computed (tools/chainbw.hip: the 8-bucket split pattern
-// moves 5.4-5.5 TB/s against 5.1-5.3 for 6-bucket runs one thread per rest entry).
+// G tables are staged packed in LDS (8 entries [q][n][x] per base offset, one
+// 16-B read per bucket half).  Persistent grid (16 waves per CU) with the next
+// two (forward) or one (backward) tiles' loads in flight while a tile is
+// computed (tools/chainbw.hip: the 8-bucket split access pattern moves 5.4-5.5
+// TB/s against 5.1-5.3 for 6-bucket runs one thread per rest entry).
 #pragma once
 #include "chain.cuh"
 
