@@ -402,8 +402,8 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     if (n_desc == 1 && BNPP_SPLIT_FLAT == 0 && FORM == kChainBwd) {
         // one bucket, backward form: the next tile's loads are issued
         // (unconditionally: the last tile is re-read rather than branching, so
-        // the wait counts stay static) before the current tile is computed; a
-        // second register set spills here (the row loads' addresses are live)
+        // the wait counts stay static) before the current tile is computed (a
+        // second tile in flight measured no faster here)
         decode(vb, in_off, out_off, gb);
         issue(in_off, rg);
         while (true) {
