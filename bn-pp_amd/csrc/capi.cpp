@@ -981,9 +981,15 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
     int rc = create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, job, 0, 1,
                         lk.owns_lock());
+    const double t1 = now_ms();
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
+    const double t2 = now_ms();
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
+    const double t3 = now_ms();
     if (job) destroy_job(job.release());
+    if (std::getenv("BNPP_TIMING"))
+        std::fprintf(stderr, "[bnpp] marginals: create %.1f ms, launch %.1f ms, run+fetch %.1f ms, free %.1f ms\n",
+                     t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
     if (rc) return rc;
     if (uptime_ms) *uptime_ms = now_ms() - t0;
     return BNPP_OK;

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <set>
 #include <thread>
 #include <climits>
@@ -1574,6 +1575,9 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                     const std::vector<int64_t> &src_sizes, int elem_bytes, int max_vec, Schedule &s,
                     std::string *msg) {
     s = Schedule{};
+    const bool timing = std::getenv("BNPP_TIMING") != nullptr;
+    auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double T0 = clk();
     s.n_src = (int)src_sizes.size();
     s.table_size = src_sizes;
     s.table_offset.assign(src_sizes.size(), -1);
@@ -1630,6 +1634,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         for (int t : dies_at[L]) arena.release(s.table_offset[t], s.table_size[t] * elem_bytes);
     }
     s.arena_bytes = arena.top;
+    const double T1 = clk();
 
     // descriptors: built in parallel (one per bucket, private dims-pool rows),
     // then grouped per level by kernel variant and concatenated
@@ -1657,6 +1662,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                  : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2)
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2) : variant_key(it.d.n_in, it.d.v1, it.d.v2);
     });
+    const double T2 = clk();
     for (const Item &it : items)
         if (!it.ok) {
             if (msg) *msg = it.msg;
@@ -1707,6 +1713,9 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         s.groups.push_back(g);
     }
     s.n_levels = n_levels;
+    if (timing)
+        std::fprintf(stderr, "[bnpp] build_schedule: lifetimes+arena %.1f ms, descriptors %.1f ms, grouping %.1f ms\n",
+                     T1 - T0, T2 - T1, clk() - T2);
     return true;
 }
 
