@@ -105,6 +105,30 @@ def test_tree_20x20_consistent_with_conditioned_partitions(ctx):
             assert abs(10 ** (lzs - lz) - marg[t][s]) < 1e-11, (t, s)
 
 
+def test_tree_32x32_full_size_consistent_with_conditioned_partitions():
+    """BASELINE config 3 at its full size (the bench's MAR instance): 32x32
+    Ising grid, column-sweep order (width 32), fp32 -- 2^32-entry messages
+    (16 GiB), the checkpointed chain schedule, split runs of 8.  The reference
+    cannot run it, so parity is through size-independent properties: every
+    marginal sums to 1, and P(x_t = s) = Z(x_t = s) / Z from conditioned
+    partitions (north-star tolerance 1e-6).  Own context, closed at the end,
+    so its ~250 GB arena does not stay cached beside the session context."""
+    c = bnpp.Context(0)
+    try:
+        m = bnpp.Model.from_dict(synth.ising_grid(32, 32, seed=0))
+        col = [r * 32 + cc for cc in range(32) for r in range(32)]
+        marg, _ = bnpp.marginals_tree(c, m, {}, "mf", bnpp.F32, order=col)
+        assert len(marg) == 1024
+        for t, p in marg.items():
+            assert len(p) == 2 and min(p) >= 0.0 and abs(sum(p) - 1.0) < 1e-6, (t, p)
+        lz = bnpp.partition(c, m, {}, "mf", bnpp.F32, order=col)[0]
+        for t in (0, 527):
+            lz0 = bnpp.partition(c, m, {t: 0}, "mf", bnpp.F32, order=col)[0]
+            assert abs(10 ** (lz0 - lz) - marg[t][0]) < 1e-6, (t, 10 ** (lz0 - lz), marg[t])
+    finally:
+        c.close()
+
+
 def test_tree_memory_budget_is_enforced(ctx):
     m = bnpp.Model.from_dict(synth.ising_grid(10, 10, seed=0))
     os.environ["BNPP_MEM_BUDGET_GB"] = "1e-7"
