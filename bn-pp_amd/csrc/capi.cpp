@@ -352,9 +352,15 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     std::vector<int64_t> src_sizes;
     for (auto &v : d.values) src_sizes.push_back((int64_t)v.size());
     std::vector<std::vector<const VEPlan *>> batches(1);
+    std::vector<int64_t> needs(plans.size());
+    parallel_for((int64_t)plans.size(), [&](int64_t i) {
+        const VEPlan &p = plans[i];
+        needs[i] = (kind == 3 ? plan_arena_bytes(p, eb) : plan_peak_bytes(p, eb)) + (int64_t)p.buckets.size() * 512;
+    });
     int64_t acc = 0;
-    for (auto &p : plans) {
-        int64_t need = (kind == 3 ? plan_arena_bytes(p, eb) : plan_peak_bytes(p, eb)) + (int64_t)p.buckets.size() * 512;
+    for (size_t i = 0; i < plans.size(); ++i) {
+        const VEPlan &p = plans[i];
+        const int64_t need = needs[i];
         if (kind == 3 && need > budget) {
             char m[256];
             std::snprintf(m, sizeof m, "bucket-tree marginals need %.2f GB, budget %.2f GB: the tree is not a "
@@ -373,8 +379,10 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     double entries = 0, moved = 0, arena = 0, levels = 0, buckets = 0;
     for (auto &bp : batches) {
         Schedule s;
+        const double tb = now_ms();
         if (!build_schedule(bp, d.cards, src_sizes, eb, max_vec_for(dtype), s, &msg))
             return set_err(BNPP_ERR_INVALID, msg);
+        if (timing) std::fprintf(stderr, "[bnpp] build_schedule call %.1f ms\n", now_ms() - tb);
         entries += s.entries;
         moved += s.elems_moved;
         arena = std::max(arena, (double)s.arena_bytes);
@@ -399,6 +407,11 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     stats[5] = (double)mx;
     stats[6] = moved * eb;
     stats[7] = (double)out.size();
+    // the plans hold millions of small vectors (per-target MAR: one plan per
+    // target); free them on the worker threads instead of one by one here
+    const double tf = now_ms();
+    parallel_for((int64_t)plans.size(), [&](int64_t i) { VEPlan dead = std::move(plans[i]); });
+    if (timing) std::fprintf(stderr, "[bnpp] plans freed in %.1f ms\n", now_ms() - tf);
     return BNPP_OK;
 }
 
