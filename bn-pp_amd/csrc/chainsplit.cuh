@@ -317,12 +317,21 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             int fixed = 0;
 #pragma unroll
             for (int p = 4; p < F; ++p) fixed += wdig(p) << p;
-            // local index e: slot 0 = bit 3 ... slot 3 = bit 0; row position: slot p at 2^p
+            // local index e: slot 0 = bit 3 ... slot 3 = bit 0; row position: slot p
+            // at 2^p, so the lane's 16 entries are the 16 consecutive positions
+            // fixed .. fixed + 15 (e bit-reversed): four 16-B reads (lane stride
+            // ROWB = 65 x 16 B: a quarter-wave covers all 64 banks once) instead
+            // of sixteen 4-B reads, which share 16 banks 4-way
+            float u[16];
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int pos = fixed + (((e >> 3) & 1) | (((e >> 2) & 1) << 1) | (((e >> 1) & 1) << 2) | ((e & 1) << 3));
-                t[e] = *reinterpret_cast<const T *>(img + lane * ROWB + 4 * pos);
+            for (int c4 = 0; c4 < 4; ++c4) {
+                const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4> *>(img + lane * ROWB + 4 * fixed + 16 * c4);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) u[4 * c4 + k] = v[k];
             }
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                t[e] = u[((e >> 3) & 1) | (((e >> 2) & 1) << 1) | (((e >> 1) & 1) << 2) | ((e & 1) << 3)];
         }
 
         // phase 1: buckets 0-3 (other slots: local bits of e, slots >= 4 from w)
