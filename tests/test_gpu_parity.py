@@ -480,6 +480,34 @@ def test_micro_bucket_checksum(ctx, k, w):
         del m_t, out
 
 
+def test_bench_bucket_full_size_exact(ctx):
+    """The bench's bucket at its full size (BASELINE config 5 restated: k = 4,
+    |S| = 14, fp32, 4^16 factor-entries, 4.3 GB in and out): checksum of
+    checksums, and 4096 sampled entries equal -- bit for bit -- to the
+    reference's arithmetic in fp32 (acc = 0; acc += m[x,s] * f[x,y] for x =
+    0..k-1, each product and sum rounded, factor.cpp:131-143, 199-205)."""
+    k, w = 4, 14
+    S = k ** w
+    g = torch.Generator(device=DEV).manual_seed(5)
+    m_t = torch.rand(k * S, generator=g, device=DEV, dtype=torch.float32) * 1.5 + 0.5
+    f_t = torch.rand(k * k, generator=g, device=DEV, dtype=torch.float32) * 1.5 + 0.5
+    out = torch.empty(S * k, device=DEV, dtype=torch.float32)
+    bnpp.bucket_eliminate(ctx, bnpp.F32, [k] * (w + 2), [m_t.data_ptr(), f_t.data_ptr()],
+                          [list(range(w + 1)), [0, w + 1]], 0, out.data_ptr(), list(range(1, w + 2)),
+                          stream=_stream())
+    torch.cuda.synchronize()
+    M, F = m_t.reshape(k, S), f_t.reshape(k, k)
+    want = (M.double().sum(1) * F.double().sum(1)).sum().item()
+    assert abs(out.double().sum().item() - want) <= 1e-4 * want
+    idx = torch.randint(0, S * k, (4096,), generator=g, device=DEV)
+    s_i, y_i = idx // k, idx % k
+    acc = torch.zeros(4096, device=DEV, dtype=torch.float32)
+    for x in range(k):
+        acc = acc + M[x, s_i] * F[x, y_i]
+    assert torch.equal(out[idx], acc)
+    del m_t, out
+
+
 def test_partition_corpus_matches_reference(ctx):
     """The reference's larger networks (Pigs, Link, Munin1-4, Barley, Mildew,
     Diabetes; with and without evidence): fp64 log10 Z against BN::partition's
