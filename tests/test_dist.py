@@ -113,16 +113,18 @@ def _tree_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_tree_part_assembly_world2():
+@pytest.mark.parametrize("world", [2, 4])
+def test_tree_part_assembly(world):
     """Chain-segment ownership of bnpp_marginals_tree_part + one all_reduce
-    assemble every marginal exactly once (gloo, world size 2)."""
+    assemble every marginal exactly once (gloo, world size 2 and 4 -- the
+    driver's scaling runs use 2, 4 and 8 ranks)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import refcpu
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_tree_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_tree_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
