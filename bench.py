@@ -162,9 +162,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BNPP_BENCH_REHEARSE=1: rehearse the N-rank path with every rank on the
+    # visible GPUs round-robin and gloo instead of RCCL (a one-GPU box checks the
+    # multi-rank logic this way; its numbers are not a measurement)
+    rehearse = os.environ.get("BNPP_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearse else "nccl")
     dev = torch.device("cuda", local)
     ctx = bnpp.Context(local)
 
