@@ -115,7 +115,8 @@ def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_or
     if os.path.exists(ref_file):
         for line in open(ref_file):
             r = json.loads(line)
-            if r.get("instance") == name and r.get("task") == "MAR" and r.get("ref_ms"):
+            if (r.get("instance") == name and r.get("task") == "MAR"
+                    and isinstance(r.get("ref_ms"), (int, float))):   # (timed-out rows hold a dict)
                 ref_ms = r["ref_ms"]
     if ref_ms:
         rec.update({"reference_cpu_ms": ref_ms,
