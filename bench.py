@@ -23,12 +23,20 @@ single core, on a bounded sample of the same bucket shape.
 32x32 Ising grid UAI (BASELINE config 3) through the checkpointed two-pass
 bucket tree (column-sweep order, width 32, fp32), split over the ranks by
 chain segments; wall-clock like the reference's uptime, warm (second call on
-the context, arena reused; "cold_wall_ms" = the first call, which maps it).
-"check": P(x_t = 0) of three targets against Z(x_t = 0) / Z from conditioned
-partitions on the same context (rank 0, after the timed calls).  The reference cannot
-run this instance (min-fill width 46), so its time is bounded from below by
-n_vars x the column-sweep PR's factor-entries at the measured cpu_baseline
-rate.  "secondary": 12x12 (reference-runnable, measured reference time).
+the context, arena reused; "cold_wall_ms" = the first call), each with its
+phase split (bnpp_last_timing).  It runs after the bucket and the CPU
+baseline: HBM freed by an earlier process is cleared by the driver in the
+background for several seconds, and a first touch before that waits for it
+(profiles/r03_cold_after_free.jsonl).  "check": P(x_t = 0) of three targets
+against Z(x_t = 0) / Z from conditioned partitions on the same context (rank
+0, after the timed calls).  The reference cannot run this instance (min-fill
+width 46), so its time is bounded from below by n_vars x the column-sweep
+PR's factor-entries at the measured cpu_baseline rate.  "secondary": 10x10
+(reference-runnable): the reference's own BN::marginals (oracle/_ref
+ref_harness mar, one core, taskset) timed in this run, beside the GPU
+per-target and bucket-tree MAR, with the largest difference between them.
+"fp64_bucket": the k=4, w=13 bucket in the reference's precision (bit-exact
+path), with its own roofline fraction.
 """
 import argparse
 import json
@@ -44,6 +52,19 @@ METRIC = "factor-entries/sec on fused product+sum-out; MAR wall-clock on 32x32 g
 HBM_PEAK = 8.0e12          # B/s, MI355X_MICROARCH.md chip table (spec)
 
 
+def host_cpu():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+
+
 def cpu_baseline(k: int, w_cpu: int, reps: int):
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
     sample = "m(x,S_1..S_%d)*f(x,y)->sum_x, k=%d, fp64, %d rep(s): %d factor-entries" % (
@@ -52,14 +73,36 @@ def cpu_baseline(k: int, w_cpu: int, reps: int):
         out = subprocess.run(["taskset", "-c", "0", harness, "micro", str(k), str(w_cpu), str(reps)],
                              capture_output=True, text=True, check=True, timeout=600).stdout
         kv = dict(line.split() for line in out.splitlines() if len(line.split()) == 2)
-        return {"value": float(kv["entries_per_s"]), "unit": "factor-entries/s", "cores": 1, "kind": "reference",
-                "sample": sample + " (reference Factor::product + sum_out, compiled from /root/reference/code)",
-                "seconds": float(kv["seconds"])}
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import refcpu
-    eps, sec = refcpu.micro_bucket(k, w_cpu, reps)
-    return {"value": eps, "unit": "factor-entries/s", "cores": 1, "kind": "port",
-            "sample": sample + " (oracle restatement)", "seconds": sec}
+        rec = {"value": float(kv["entries_per_s"]), "unit": "factor-entries/s", "cores": 1, "kind": "reference",
+               "sample": sample + " (reference Factor::product + sum_out, compiled from /root/reference/code; "
+                                  "taskset -c 0)", "seconds": float(kv["seconds"])}
+    else:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import refcpu
+        eps, sec = refcpu.micro_bucket(k, w_cpu, reps)
+        rec = {"value": eps, "unit": "factor-entries/s", "cores": 1, "kind": "port",
+               "sample": sample + " (oracle restatement)", "seconds": sec}
+    rec.update(host_cpu())
+    return rec
+
+
+def reference_mar(name: str):
+    """The reference's own BN::marginals on a bundled instance (per-target VE,
+    model.cpp:326-334, min-fill), one core: (uptime ms, {var: [p..]}) or None."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    path = os.path.join(REPO, "tests", "golden", "models", name)
+    out = subprocess.run(["taskset", "-c", "0", harness, "mar", path, "-", "mf"], capture_output=True, text=True,
+                         check=True, timeout=600).stdout
+    marg, up = {}, None
+    for line in out.splitlines():
+        if line.startswith("M") and "|" in line:
+            head, _, vals = line.split("|")
+            marg[int(head.split()[0][1:])] = [float(x) for x in vals.split()]
+        elif line.startswith("uptime_ms"):
+            up = float(line.split()[1])
+    return up, marg
 
 
 def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_order):
@@ -92,12 +135,15 @@ def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_or
     # cold: the first call on the context (plans, allocates the arena, loads kernels);
     # warm: the same call again, arena reused (a serving process keeps it)
     marg, cold_ms = timed()
+    cold_phases = bnpp.last_timing()
     marg2, ms = timed()
+    warm_phases = bnpp.last_timing()
     assert marg2 == marg
     name = "ising%dx%d" % (rows, cols)
     rec = {"instance": "%s all marginals, bucket tree, %s order, %s" % (
                name, "column-sweep (width %d)" % rows if column_order else "min-fill", dtype_name),
            "wall_ms": ms, "cold_wall_ms": cold_ms, "n_gpus": world, "p_var0": marg[0],
+           "phases_ms": {"cold": cold_phases, "warm": warm_phases},
            "max_sum_err": max(abs(sum(p) - 1.0) for p in marg.values())}
     if rank == 0:
         # P(x_t = 0) = Z(x_t = 0) / Z, each Z by one conditioned VE (BN::partition)
@@ -110,23 +156,40 @@ def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_or
         rec["check"] = {"method": "P(x_t=0) vs Z(x_t=0)/Z from conditioned partitions", "abs_err": errs,
                         "max_abs_err": max(errs.values()), "tolerance": tol,
                         "ok": max(errs.values()) <= tol}
-    ref_file = os.path.join(REPO, "profiles", "r01_ve_bench.jsonl")
-    ref_ms = None
-    if os.path.exists(ref_file):
-        for line in open(ref_file):
-            r = json.loads(line)
-            if (r.get("instance") == name and r.get("task") == "MAR"
-                    and isinstance(r.get("ref_ms"), (int, float))):   # (timed-out rows hold a dict)
-                ref_ms = r["ref_ms"]
-    if ref_ms:
-        rec.update({"reference_cpu_ms": ref_ms,
-                    "reference_cpu_source": "profiles/r01_ve_bench.jsonl (oracle/_ref ref_harness mar, 1 core)",
-                    "speedup_vs_reference": ref_ms / ms})
-    else:
-        # the reference cannot run it (min-fill width 46 at 32x32); lower bound
-        # (filled in by reference_bound once the CPU rate is measured): one VE
-        # per variable, each at least the column-sweep PR's factor-entries
-        rec["_bound"] = (m.n_vars, bnpp.plan_stats(m, 0, {}, "mf", dtype=dt, order=order)[0], rows)
+    # the reference cannot run it (min-fill width 46 at 32x32); lower bound
+    # (filled in by reference_bound once the CPU rate is measured): one VE
+    # per variable, each at least the column-sweep PR's factor-entries
+    rec["_bound"] = (m.n_vars, bnpp.plan_stats(m, 0, {}, "mf", dtype=dt, order=order)[0], rows)
+    return rec
+
+
+def secondary_mar(ctx, name: str, with_reference: bool):
+    """A reference-runnable MAR (min-fill, fp64): the GPU per-target VE (the
+    reference's algorithm, bit-exact path) and the GPU bucket tree, each warm
+    (second call), and -- rank 0 at N=1 -- the reference's own BN::marginals
+    timed in this run on one core."""
+    import bnpp
+    m = bnpp.Model.load(os.path.join(REPO, "tests", "golden", "models", name))
+    rec = {"instance": "%s all marginals, min-fill, f64" % name}
+    res = {}
+    for kind, fn in (("per_target", lambda: bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)),
+                     ("bucket_tree", lambda: bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64))):
+        fn()
+        t0 = time.perf_counter()
+        res[kind], _ = fn()
+        rec[kind + "_wall_ms"] = (time.perf_counter() - t0) * 1e3
+    rec["max_abs_diff_tree_vs_per_target"] = max(abs(a - b) for t in res["per_target"]
+                                                 for a, b in zip(res["per_target"][t], res["bucket_tree"][t]))
+    if with_reference:
+        r = reference_mar(name)
+        if r is not None:
+            up, rm = r
+            rec.update({"reference_cpu_ms": up, "reference_kind": "reference (oracle/_ref ref_harness mar, "
+                                                                  "compiled from /root/reference/code, taskset -c 0)",
+                        "speedup_per_target": up / rec["per_target_wall_ms"],
+                        "speedup_bucket_tree": up / rec["bucket_tree_wall_ms"],
+                        "max_abs_diff_vs_reference": max(abs(a - b) for t in rm
+                                                         for a, b in zip(rm[t], res["per_target"][t]))})
     return rec
 
 
@@ -138,6 +201,47 @@ def reference_bound(rec, cpu_rate):
     rec.update({"reference_cpu_lower_bound_s": lb, "speedup_vs_reference_lower_bound": lb * 1e3 / rec["wall_ms"],
                 "reference_note": "reference MAR = one VE per variable (model.cpp:326-334); bound = n_vars x "
                                   "factor-entries of the width-%d column-sweep PR / measured cpu_baseline rate" % rows})
+
+
+def fp64_bucket(ctx, dev, stream, rank, k=4, w=13, steps=10):
+    """The bench bucket in fp64 (the reference's arithmetic; bit-exact against
+    it): m(x, S_1..S_w) * f(x, y) -> sum_x, timed with HIP events on the
+    launch stream, with an exact spot check against the same sums in torch."""
+    import torch
+    import bnpp
+    S = k ** w
+    g = torch.Generator(device=dev).manual_seed(4321 + rank)
+    m_t = torch.rand(k * S, generator=g, device=dev, dtype=torch.float64) * 1.5 + 0.5
+    f_t = torch.rand(k * k, generator=g, device=dev, dtype=torch.float64) * 1.5 + 0.5
+    out = torch.empty(S * k, device=dev, dtype=torch.float64)
+    cards = [k] * (w + 2)
+
+    def step():
+        bnpp.bucket_eliminate(ctx, bnpp.F64, cards, [m_t.data_ptr(), f_t.data_ptr()], [list(range(w + 1)), [0, w + 1]],
+                              0, out.data_ptr(), list(range(1, w + 2)), stream=stream.cuda_stream)
+    for _ in range(3):
+        step()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for i in range(steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    alg = 8 * (k * S + k * k + S * k)
+    gs = torch.Generator(device=dev).manual_seed(77 + rank)
+    idx = torch.randint(0, S * k, (512,), generator=gs, device=dev)
+    s_i, y_i = idx // k, idx % k
+    M, F = m_t.reshape(k, S), f_t.reshape(k, k)
+    acc = torch.zeros(512, device=dev, dtype=torch.float64)
+    with torch.cuda.stream(stream):
+        for x in range(k):
+            acc = acc + M[x, s_i] * F[x, y_i]
+    torch.cuda.synchronize(dev)
+    return {"workload": "potts-k%d bucket m(x,S_1..S_%d)*f(x,y)->sum_x, f64" % (k, w),
+            "factor_entries_per_s": float(k ** (w + 2)) / (kern_ms * 1e-3), "kernel_ms": kern_ms,
+            "alg_bytes_per_launch": alg, "achieved_GBps": alg / (kern_ms * 1e-3) / 1e9,
+            "frac": alg / (kern_ms * 1e-3) / HBM_PEAK, "spot_check_exact": bool(torch.equal(out[idx], acc))}
 
 
 def main():
@@ -152,6 +256,7 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-mar", action="store_true")
+    ap.add_argument("--no-fp64", action="store_true")
     ap.add_argument("--mar-rows", type=int, default=32)
     ap.add_argument("--mar-cols", type=int, default=32)
     args = ap.parse_args()
@@ -175,14 +280,6 @@ def main():
     dev = torch.device("cuda", local)
     ctx = bnpp.Context(local)
 
-    # MAR first, in a fresh process: its cold call maps fresh HBM pages (after a
-    # free the driver clears the returned pages first, ~0.5 s); the context
-    # keeps the arena, the bucket below fits beside it
-    mar = None
-    if not args.no_mar:
-        d = dist if world > 1 else None
-        mar = mar_wallclock(ctx, rank, world, d, dev, args.mar_rows, args.mar_cols, "f32", True)
-        mar["secondary"] = mar_wallclock(ctx, rank, world, d, dev, 12, 12, "f64", False)
     dt = bnpp.F32 if args.dtype == "f32" else bnpp.F64
     tdt = torch.float32 if dt == bnpp.F32 else torch.float64
     eb = 4 if dt == bnpp.F32 else 8
@@ -249,6 +346,13 @@ def main():
     spot_ok = bool(torch.equal(out[idx], acc))
     ok = ok and spot_ok
 
+    fp64 = None
+    if not args.no_fp64:
+        fp64 = fp64_bucket(ctx, dev, stream, rank)
+    del m_t, f_t, out, M, F, acc, idx, s_i, y_i
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+
     traffic = None
     tpath = os.path.join(REPO, "profiles", "traffic_r02.json")   # tools/profile_bench.sh, this kernel
     if os.path.exists(tpath):
@@ -260,10 +364,15 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(k, args.cpu_w, args.cpu_reps)
 
-    if mar is not None:
-        for rec in (mar, mar["secondary"]):
-            if "_bound" in rec:
-                reference_bound(rec, cpu["value"] if cpu else 7.2e6)   # r01 cpu_baseline when not run here
+    # MAR after the bucket and the CPU baseline (see the module docstring: HBM
+    # another process freed is cleared in the background for several seconds)
+    mar = None
+    if not args.no_mar:
+        d = dist if world > 1 else None
+        mar = mar_wallclock(ctx, rank, world, d, dev, args.mar_rows, args.mar_cols, "f32", True)
+        reference_bound(mar, cpu["value"] if cpu else 7.2e6)   # r01 cpu_baseline when not run here
+        if rank == 0:
+            mar["secondary"] = secondary_mar(ctx, "ising10x10.uai", world == 1 and not args.no_cpu)
 
     if rank == 0:
         line = {
@@ -287,6 +396,7 @@ def main():
                          "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "mar": mar,
+            "fp64_bucket": fp64,
             "checksum_ok": ok,
             "spot_check_exact": spot_ok,
         }
@@ -294,6 +404,8 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     if mar and "check" in mar and not mar["check"]["ok"]:
+        ok = False
+    if fp64 is not None and not fp64["spot_check_exact"]:
         ok = False
     if not ok:
         sys.exit(3)

@@ -28,6 +28,7 @@ bnpp_ctx *ctx() {
             const char *e = std::getenv("BNPP_DEVICE");
             dev = e ? std::atoi(e) : 0;
         }
+        if (!bnpp_abi_matches()) throw std::runtime_error("bnpp: libbnpp ABI version differs from include/bnpp.h");
         if (bnpp_ctx_create(dev, &g_ctx) != BNPP_OK)
             throw std::runtime_error(std::string("bnpp: cannot create a GPU context: ") + bnpp_last_error());
     }

@@ -25,6 +25,8 @@
 
 using namespace bnpp;
 
+constexpr int kTimingPhases = 8;
+
 struct bnpp_ctx {
     Context c;
     std::mutex cache_mu;            // one one-shot call at a time uses c.arena_cache
@@ -46,6 +48,8 @@ struct bnpp_job {
 namespace {
 
 thread_local std::string g_err;
+// phase split of this thread's last partition / marginals call (bnpp_last_timing)
+thread_local double g_timing[kTimingPhases] = {0};
 
 int set_err(int status, const std::string &msg) {
     g_err = msg;
@@ -184,6 +188,13 @@ uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<i
     mix((uint64_t)chain_eb);              // fused runs on/off change the plan
     mix((uint64_t)part);
     mix((uint64_t)n_parts);
+    // the planner's tuning knobs change the plan and its arena need
+    for (const char *k : {"BNPP_NO_SPLIT", "BNPP_SPLIT_MIN_F", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_NO_REDUCE_MANY",
+                          "BNPP_CHAIN_RUN_MAX", "BNPP_NO_CHAIN_FWDV", "BNPP_NO_STREAM", "BNPP_NO_SLAB", "BNPP_MAX_TILE"}) {
+        const char *v = std::getenv(k);
+        mix(0x9e37u);
+        for (const char *c = v ? v : ""; *c; ++c) mix((unsigned char)*c);
+    }
     return h;
 }
 
@@ -244,7 +255,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
         plans.push_back(plan_bucket_tree(d.cards, views, ord, targets, part, n_parts));
-        auto need = [&](const VEPlan &p) { return plan_arena_bytes(p, eb) + (int64_t)p.buckets.size() * 512; };
+        auto need = [&](const VEPlan &p) { return sat_add(plan_arena_bytes(p, eb), (int64_t)p.buckets.size() * 512); };
         const char *force = std::getenv("BNPP_TREE_SLOTS");     // testing / tuning: chain mode, fixed slots
         if (force && std::atoi(force) > 0) {
             std::string msg;
@@ -355,7 +366,7 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     std::vector<int64_t> needs(plans.size());
     parallel_for((int64_t)plans.size(), [&](int64_t i) {
         const VEPlan &p = plans[i];
-        needs[i] = (kind == 3 ? plan_arena_bytes(p, eb) : plan_peak_bytes(p, eb)) + (int64_t)p.buckets.size() * 512;
+        needs[i] = sat_add(kind == 3 ? plan_arena_bytes(p, eb) : plan_peak_bytes(p, eb), (int64_t)p.buckets.size() * 512);
     });
     int64_t acc = 0;
     for (size_t i = 0; i < plans.size(); ++i) {
@@ -367,12 +378,12 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
                           "chain or no checkpoint count fits (per-target marginals or a narrower order)", need / 1e9, budget / 1e9);
             return set_err(BNPP_ERR_OOM, m);
         }
-        if (!batches.back().empty() && acc + need > budget) {
+        if (!batches.back().empty() && sat_add(acc, need) > budget) {
             batches.emplace_back();
             acc = 0;
         }
         batches.back().push_back(&p);
-        acc += need;
+        acc = sat_add(acc, need);
     }
     out.clear();
     std::string msg;
@@ -381,7 +392,7 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
         Schedule s;
         const double tb = now_ms();
         if (!build_schedule(bp, d.cards, src_sizes, eb, max_vec_for(dtype), s, &msg))
-            return set_err(BNPP_ERR_INVALID, msg);
+            return set_err(s.arena_bytes >= kSatMax ? BNPP_ERR_OOM : BNPP_ERR_INVALID, msg);
         if (timing) std::fprintf(stderr, "[bnpp] build_schedule call %.1f ms\n", now_ms() - tb);
         entries += s.entries;
         moved += s.elems_moved;
@@ -453,6 +464,7 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     }
     std::vector<Schedule> batches;
     if (n_parts < 1 || part < 0 || part >= n_parts) return set_err(BNPP_ERR_INVALID, "bad part / n_parts");
+    const double tp = now_ms();
     int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, memory_budget(ctx, use_cache),
                             batches, job->stats, part, n_parts);
     if (rc) return rc;
@@ -462,6 +474,10 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     const double t1 = now_ms();
     rc = make_program(ctx->c, job->src, std::move(batches), job->pg, use_cache);
     if (rc) return from_ctx(ctx, rc);
+    g_timing[0] = t0 - tp;
+    g_timing[1] = t1 - t0;
+    g_timing[2] = now_ms() - t1;
+    g_timing[7] = job->pg.arena_cached && use_cache ? 1.0 : 0.0;
     if (std::getenv("BNPP_TIMING"))
         std::fprintf(stderr, "[bnpp] job: upload %.1f ms, program (arena %.2f GB) %.1f ms\n", t1 - t0,
                      job->pg.arena_bytes / 1e9, now_ms() - t1);
@@ -519,6 +535,14 @@ int job_results(bnpp_job *job, hipStream_t stream, double *out, double *z_out, i
     return BNPP_OK;
 }
 
+// launch / run+fetch / free / total of a call whose create_job filled phases 0-2
+void record_call_timing(double t0, double t1, double t2, double t3) {
+    g_timing[3] = t2 - t1;
+    g_timing[4] = t3 - t2;
+    g_timing[5] = now_ms() - t3;
+    g_timing[6] = now_ms() - t0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -537,6 +561,12 @@ const char *bnpp_strerror(int status) {
 }
 
 const char *bnpp_last_error(void) { return g_err.c_str(); }
+
+int bnpp_last_timing(double *out, int n) {
+    if (!out || n < 0) return set_err(BNPP_ERR_INVALID, "null output");
+    for (int i = 0; i < n && i < kTimingPhases; ++i) out[i] = g_timing[i];
+    return BNPP_OK;
+}
 int bnpp_version(void) { return BNPP_VERSION; }
 
 int bnpp_device_count(int *n) {
@@ -972,10 +1002,14 @@ int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
     int rc = create_job(ctx, m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype, job, 0, 1,
                         lk.owns_lock());
+    const double t1 = now_ms();
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
+    const double t2 = now_ms();
     double lz = 0, zz = 0;
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, &lz, &zz);
+    const double t3 = now_ms();
     if (job) destroy_job(job.release());
+    record_call_timing(t0, t1, t2, t3);
     if (rc) return rc;
     if (log10_z) *log10_z = lz;
     if (z) *z = zz;
@@ -1000,6 +1034,7 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
     const double t3 = now_ms();
     if (job) destroy_job(job.release());
+    record_call_timing(t0, t1, t2, t3);
     if (std::getenv("BNPP_TIMING"))
         std::fprintf(stderr, "[bnpp] marginals: create %.1f ms, launch %.1f ms, run+fetch %.1f ms, free %.1f ms\n",
                      t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
@@ -1034,6 +1069,7 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
     if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr, owned);
     const double t3 = now_ms();
     if (job) destroy_job(job.release());
+    record_call_timing(t0, t1, t2, t3);
     if (timing)
         std::fprintf(stderr, "[bnpp] tree marginals: create %.1f ms, launch %.1f ms, run+fetch %.1f ms, free %.1f ms\n",
                      t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);

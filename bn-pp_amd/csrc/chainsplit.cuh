@@ -29,6 +29,12 @@
 #pragma once
 #include "chain.cuh"
 
+// The split forms need the 160-KiB dynamic-LDS opt-in of gfx950 (CDNA4); the
+// planner emits them unconditionally, so any other target must not build.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "chainsplit.cuh: split chain runs need gfx950 (160 KiB LDS per workgroup)"
+#endif
+
 #include <mutex>
 
 namespace bnpp {

@@ -42,14 +42,14 @@ std::vector<int64_t> natural_strides(const std::vector<int> &vars, const std::ve
     int64_t acc = 1;
     for (int i = (int)vars.size() - 1; i >= 0; --i) {
         s[i] = acc;
-        acc *= cards[vars[i]];
+        acc = sat_mul(acc, cards[vars[i]]);
     }
     return s;
 }
 
 int64_t table_size(const std::vector<int> &vars, const std::vector<int> &cards) {
     int64_t s = 1;
-    for (int v : vars) s *= cards[v];
+    for (int v : vars) s = sat_mul(s, cards[v]);
     return s;
 }
 
@@ -194,10 +194,13 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         md.push_back(r);
     }
     int64_t rest = 1;
-    for (const RDim &r : md) rest *= (int64_t)r.card;
+    for (const RDim &r : md) rest = sat_mul(rest, (int64_t)r.card);
+    if (rest >= (kSatMax >> 8)) return fail("chain: message beyond any device");
     // kernel form
     int form = 0, V = 1;
     bool fwd_v = false;
+    bool fwd = false, bwd = false;                    // one-thread forms fit (the split forms' fallbacks)
+    int bv = 1;
     if (sum) {
         // summing run: the thread's V rest entries are contiguous in the input
         // (vector loads, one per slot assignment) and in the output
@@ -211,16 +214,16 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         if (!ok) return fail("chain: summing run layout fits no kernel form");
         form = kChainSum;
     } else {
-        bool fwd = N * eb <= 256;                    // rows staged through LDS in 128-B parts
+        fwd = N * eb <= 256;                         // rows staged through LDS in 128-B parts
         for (int p = 0; fwd && p < F; ++p) {
             int64_t pl = 1;
             for (int q = p + 1; q < F; ++q) pl *= K;
             fwd = os[p] == pl;
         }
         if (fwd && !md.empty()) fwd = md[0].out == N;
-        bool bwd = true;
+        bwd = true;
         const int W = eb == 4 ? (N % 4 == 0 ? 4 : N % 2 == 0 ? 2 : 1) : (N % 2 == 0 ? 2 : 1);   // load_n width
-        const int bv = chain_bwd_v(N, eb);
+        bv = chain_bwd_v(N, eb);
         int64_t pk = 1;
         for (int p = 0; bwd && p < F; ++p, pk *= K) bwd = is[p] == pk;
         bwd = bwd && !md.empty() && md[0].out == 1 && md[0].card % (uint64_t)bv == 0 && big.base % W == 0;
@@ -281,8 +284,15 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     if (chain_split_form(form) && (dep == kDepAny || !pk_fits)) {
         if (N > 64) return fail(pk_fits ? "chain: split form needs G_j to depend on one neighbouring slot"
                                         : "chain: packed G tables exceed the split form's LDS");
-        form = form == kChainFwdS ? kChainFwd : kChainBwd;             // the one-thread form, as before
-        if (form == kChainBwd) V = chain_bwd_v(N, eb);
+        // the one-thread form, only where its own layout conditions hold
+        if (form == kChainFwdS) {
+            if (!fwd) return fail("chain: split forward run falls back to a layout the one-thread form rejects");
+            form = kChainFwd;
+        } else {
+            if (!bwd) return fail("chain: split backward run falls back to a layout the one-thread form rejects");
+            form = kChainBwd;
+            V = bv;
+        }
     }
     if (fwd_v && !std::getenv("BNPP_NO_CHAIN_FWDV") && chain_supported(eb, chain_key(kChainFwdV, K, F, dep))) {
         form = kChainFwdV;
@@ -400,7 +410,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
             if (msg) *msg = "cardinality must be >= 1";
             return false;
         }
-        out_size *= c;
+        out_size = sat_mul(out_size, (int64_t)c);
         if (c == 1) continue;
         Dim dm;
         dm.card = (uint64_t)c;
@@ -423,6 +433,10 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
             if (ok) bk.card *= dm.card;
         }
         if (!ok) merged.push_back(dm);
+    }
+    if (out_size >= (kSatMax >> 6)) {
+        if (msg) *msg = "bucket output beyond any device";
+        return false;
     }
     std::vector<int64_t> out_strides;     // kOutStrided: output stride per (permuted) dim
     int k = 1;
@@ -1472,13 +1486,13 @@ int64_t plan_peak_bytes(const VEPlan &p, int elem_bytes) {
         if (r >= 0) last[r] = p.n_levels + 1;
     std::vector<int64_t> delta(p.n_levels + 3, 0);
     for (int t = p.n_src; t < nt; ++t) {
-        int64_t bytes = ((p.msgs[t - p.n_src].size * elem_bytes + 255) / 256) * 256;
-        delta[born[t]] += bytes;
+        const int64_t bytes = sat_add(sat_mul(p.msgs[t - p.n_src].size, elem_bytes), 255) / 256 * 256;
+        delta[born[t]] = sat_add(delta[born[t]], bytes);
         delta[std::max(last[t], born[t]) + 1] -= bytes;
     }
     int64_t live = 0, peak = 0;
     for (int64_t d : delta) {
-        live += d;
+        live = sat_add(live, d);
         peak = std::max(peak, live);
     }
     return peak;
@@ -1494,6 +1508,9 @@ struct Arena {
     std::pmr::map<int64_t, int64_t> free_{&pool_};            // offset -> length
     std::pmr::set<std::pair<int64_t, int64_t>> by_len_{&pool_};   // (length, offset)
     int64_t top = 0;
+    // a plan beyond any device (sizes saturated at kSatMax): stop placing
+    // tables (offsets would collide at the saturated top), report kSatMax
+    bool saturated = false;
     void add_free(int64_t off, int64_t len) {
         free_[off] = len;
         by_len_.insert({len, off});
@@ -1503,6 +1520,11 @@ struct Arena {
         free_.erase(it);
     }
     int64_t alloc(int64_t n) {
+        if (saturated || n >= kSatMax / 4 || top >= kSatMax / 4) {
+            saturated = true;
+            top = kSatMax;
+            return 0;
+        }
         n = (n + 255) & ~(int64_t)255;
         // best fit: the smallest free block that holds n, lowest offset among
         // equals (small temporaries go into small holes instead of splitting
@@ -1529,6 +1551,7 @@ struct Arena {
         return off;
     }
     void release(int64_t off, int64_t n) {
+        if (saturated) return;
         n = (n + 255) & ~(int64_t)255;
         auto nx = free_.lower_bound(off);
         if (nx != free_.end() && off + n == nx->first) {     // merge the next block
@@ -1568,7 +1591,7 @@ int64_t plan_arena_bytes(const VEPlan &p, int elem_bytes) {
     }
     Arena arena;
     std::vector<int64_t> off(nt, 0);
-    auto bytes = [&](int t) { return p.msgs[t - p.n_src].size * elem_bytes; };
+    auto bytes = [&](int t) { return sat_mul(p.msgs[t - p.n_src].size, elem_bytes); };
     for (int L = 1; L <= p.n_levels; ++L) {
         for (int t : born_at[L]) off[t] = arena.alloc(bytes(t));
         for (int t : dies_at[L]) arena.release(off[t], bytes(t));
@@ -1636,10 +1659,14 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     const double Tl = clk();
     Arena arena;
     for (int L = 1; L <= n_levels; ++L) {
-        for (int t : born_at[L]) s.table_offset[t] = arena.alloc(s.table_size[t] * elem_bytes);
-        for (int t : dies_at[L]) arena.release(s.table_offset[t], s.table_size[t] * elem_bytes);
+        for (int t : born_at[L]) s.table_offset[t] = arena.alloc(sat_mul(s.table_size[t], elem_bytes));
+        for (int t : dies_at[L]) arena.release(s.table_offset[t], sat_mul(s.table_size[t], elem_bytes));
     }
     s.arena_bytes = arena.top;
+    if (arena.saturated) {                   // tables of 2^58+ bytes: no descriptors for those
+        if (msg) *msg = "the plan's tables exceed any device (more than 2^58 bytes); use a narrower elimination order";
+        return false;
+    }
     const double T1 = clk();
 
     // descriptors: built in parallel (one per bucket, private dims-pool rows),

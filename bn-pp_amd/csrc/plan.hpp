@@ -23,6 +23,18 @@ struct View {
 };
 
 // Row-major strides, last variable fastest (domain.cpp:15-26).
+// Sizes, strides and byte counts saturate at kSatMax (2^60): a min-fill order
+// on a large grid plans tables of 2^100+ entries that no device could hold;
+// they must compare as "too big" against any memory budget, not overflow.
+constexpr int64_t kSatMax = (int64_t)1 << 60;
+inline int64_t sat_mul(int64_t a, int64_t b) {
+    int64_t r;
+    return __builtin_mul_overflow(a, b, &r) || r > kSatMax ? kSatMax : r;
+}
+inline int64_t sat_add(int64_t a, int64_t b) {
+    int64_t r;
+    return __builtin_add_overflow(a, b, &r) || r > kSatMax ? kSatMax : r;
+}
 std::vector<int64_t> natural_strides(const std::vector<int> &vars, const std::vector<int> &cards);
 int64_t table_size(const std::vector<int> &vars, const std::vector<int> &cards);
 View natural_view(int table, const std::vector<int> &vars, const std::vector<int> &cards);

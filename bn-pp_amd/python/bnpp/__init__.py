@@ -41,6 +41,7 @@ _SIGS = {
     "bnpp_strerror": (C.c_char_p, [_I]),
     "bnpp_last_error": (C.c_char_p, []),
     "bnpp_version": (_I, []),
+    "bnpp_last_timing": (_I, [_DP, _I]),
     "bnpp_device_count": (_I, [_IP]),
     "bnpp_ctx_create": (_I, [_I, C.POINTER(_P)]),
     "bnpp_ctx_destroy": (_I, [_P]),
@@ -85,6 +86,13 @@ for _name, (_res, _args) in _SIGS.items():
 
 EXPORTED = sorted(_SIGS)
 
+# The signature table above is for this ABI version (include/bnpp.h
+# BNPP_VERSION); a library of another version would take shifted arguments.
+ABI_VERSION = 200
+if _lib.bnpp_version() != ABI_VERSION:
+    raise ImportError("libbnpp.so ABI version %d, this binding expects %d (%s)"
+                      % (_lib.bnpp_version(), ABI_VERSION, LIB_PATH))
+
 
 class BnppError(RuntimeError):
     def __init__(self, status: int, where: str):
@@ -105,6 +113,17 @@ def _ints(xs: Iterable[int]):
 def _dbls(xs: Iterable[float]):
     xs = list(xs)
     return (C.c_double * max(len(xs), 1))(*xs)
+
+
+TIMING_PHASES = ("plan_ms", "upload_ms", "program_ms", "launch_ms", "run_fetch_ms", "free_ms", "total_ms",
+                 "arena_reused")
+
+
+def last_timing() -> Dict[str, float]:
+    """Phase split of this thread's last partition / marginals call (bnpp_last_timing)."""
+    out = (C.c_double * 8)()
+    _check(_lib.bnpp_last_timing(out, 8), "bnpp_last_timing")
+    return dict(zip(TIMING_PHASES, list(out)))
 
 
 def device_count() -> int:

@@ -57,6 +57,19 @@ enum bnpp_heuristic { BNPP_ORDER_GIVEN = 0, BNPP_MIN_FILL = 1, BNPP_WEIGHTED_MIN
 const char *bnpp_strerror(int status);
 const char *bnpp_last_error(void);
 int bnpp_version(void);
+/* 1 when the loaded library speaks the ABI this header declares.  Callers
+ * check it once: a library of another version links (the symbol names are
+ * unchanged) but would read shifted arguments. */
+static inline int bnpp_abi_matches(void) { return bnpp_version() == BNPP_VERSION; }
+/* Phase split (ms) of this thread's last bnpp_partition / bnpp_marginals /
+ * bnpp_marginals_tree[_part] call -- the reference times these tasks as one
+ * "uptime" (model.cpp:258/296, 309/343):
+ *   out[0] ordering + planning + schedule (host)   out[1] source upload
+ *   out[2] device program (arena, descriptors)     out[3] launch enqueue
+ *   out[4] device run + result fetch                out[5] free
+ *   out[6] total                                    out[7] 1 if the context's cached arena was reused
+ * Writes min(n, 8) values. */
+int bnpp_last_timing(double *out, int n);
 
 /* ------------------------------------------------------------- device */
 typedef struct bnpp_ctx bnpp_ctx;

@@ -7,15 +7,18 @@
 // have external linkage in io.cpp:43-100 but are not declared in io.hh.
 //
 //   pr    <uai> <evid|-> <given|mf|wmf|md>     BN::partition (model.cpp:250)
-//   mar   <uai> <evid|-> <given|mf|wmf|md>     per-target BN::variable_elimination
+//   mar   <uai> <evid|-> <given|mf|wmf|md> [t..] per-target BN::variable_elimination
 //                                              + normalize (model.cpp:326-334),
 //                                              evidence vars left out of the order
-//                                              (dodges the -mar -mf crash)
+//                                              (dodges the -mar -mf crash);
+//                                              optional target ids: only those
 //   ve    <uai> <evid|-> v1 v2 ...             VE with an explicit order
 //   width <uai> <mf|wmf|md>                    Graph::ordering induced width
 //   kat   <opfile>                             single Factor ops (product, sum_out, ...)
 //   micro <k> <w> <reps>                       m(x,S)*f(x,y) -> sum_x, timed
 //   sp    <uai> [max] [eps]                    loopy BP (FactorGraph, graph.cpp:256-403)
+//   query <uai> <given|mf|wmf|md> <queryfile>  BN::query_ve (model.cpp:204-248) for every
+//                                              `query T | E` line (REPL syntax, bn.cpp:263)
 #include "variable.hh"
 #include "domain.hh"
 #include "factor.hh"
@@ -34,6 +37,7 @@
 #include <sstream>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace bn {
@@ -101,7 +105,10 @@ int main(int argc, char **argv) {
         auto t0 = std::chrono::steady_clock::now();
         std::vector<const Factor *> fs;
         for (auto pf : m->factors()) fs.push_back(new Factor(pf->conditioning(ev)));
-        for (auto pv : m->variables()) {
+        std::vector<const Variable *> targets;
+        for (int i = 5; i < argc; ++i) targets.push_back(m->variables().at(std::atoi(argv[i])));
+        if (targets.empty()) targets.assign(m->variables().begin(), m->variables().end());
+        for (auto pv : targets) {
             std::vector<const Variable *> vars;
             for (auto pv2 : m->variables())
                 if (pv2 != pv && !ev.count(pv2->id())) vars.push_back(pv2);
@@ -225,6 +232,38 @@ int main(int argc, char **argv) {
             print_factor(tag, marg[i]);
         }
         std::printf("uptime_ms %.6f\n", std::chrono::duration<double, std::milli>(t1 - t0).count());
+        delete m;
+        return 0;
+    }
+    if (cmd == "query" && argc >= 5) {
+        BN *m = load(argv[2]);
+        auto o = opts_for(argv[3]);
+        std::ifstream in(argv[4]);
+        std::string line;
+        int qi = 0;
+        auto ids = [&](std::string s) {
+            std::unordered_set<const Variable *> out;
+            for (char &c : s)
+                if (c == ',') c = ' ';
+            std::istringstream ss(s);
+            unsigned id;
+            while (ss >> id) out.insert(m->variables().at(id));
+            return out;
+        };
+        while (std::getline(in, line)) {
+            if (line.compare(0, 6, "query ") != 0) continue;
+            std::string body = line.substr(6), t = body, e;
+            size_t bar = body.find('|');
+            if (bar != std::string::npos) {
+                t = body.substr(0, bar);
+                e = body.substr(bar + 1);
+            }
+            double up = 0;
+            Factor q = m->query_ve(ids(t), ids(e), o, up);
+            char tag[32];
+            std::snprintf(tag, sizeof tag, "Q%d", qi++);
+            print_factor(tag, q);
+        }
         delete m;
         return 0;
     }

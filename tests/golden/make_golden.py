@@ -6,6 +6,9 @@ Run in the build container (needs /root/reference and `make -C oracle ref`):
     python tests/golden/make_golden.py          # everything
     python tests/golden/make_golden.py sp       # loopy BP fixtures only (sp_golden.json)
     python tests/golden/make_golden.py corpus   # larger networks' PR (corpus_golden.json)
+    python tests/golden/make_golden.py config4  # noisy-OR 50x80, width 22 (config4_golden.json)
+    python tests/golden/make_golden.py cli      # reference bn / mn stdout (cli_golden.json)
+    python tests/golden/make_golden.py query    # BN::query_ve answers (query_golden.json)
 
 It
   1. copies the reference's own model + fixture files that the tests use into
@@ -336,8 +339,142 @@ def corpus_golden():
         json.dump({"cases": cases}, f, indent=1)
 
 
+# BASELINE config 4 at its stated size: a two-layer noisy-OR
+# BN, 50 diseases -> 80 findings (3 parents each), every finding observed;
+# reference min-fill width 22.  Reference PR (BN::partition, model.cpp:250-301),
+# three single-target conditionings Z(x_t = s), and the reference MAR of every
+# disease (one VE per target, model.cpp:326-334), run as 8 parallel processes.
+C4_MODEL = "noisyor_50_80.uai"
+C4_TARGETS = (0, 24, 49)
+
+
+def config4_golden():
+    from concurrent.futures import ThreadPoolExecutor
+    md = synth.noisy_or_bn(50, 80, 3, seed=0)
+    synth.write_uai(md, model_path(C4_MODEL))
+    rng = random.Random(50)
+    ev = {v: rng.randrange(2) for v in range(50, 130)}
+    synth.write_evidence(ev, model_path(C4_MODEL + ".evid"))
+    path, evp = model_path(C4_MODEL), model_path(C4_MODEL + ".evid")
+    cond_files = []
+    for t in C4_TARGETS:
+        e = dict(ev)
+        e[t] = 1
+        name = "/tmp/%s.t%d.evid" % (C4_MODEL, t)
+        synth.write_evidence(e, name)
+        cond_files.append((t, name))
+
+    def job(spec):
+        kind, arg = spec
+        if kind == "pr":
+            return spec, parse_kv(run("pr", path, arg, "mf", timeout=3600))
+        return spec, run("mar", path, evp, "mf", *arg, timeout=3600)
+
+    specs = [("pr", evp)] + [("pr", f) for _, f in cond_files]
+    diseases = list(range(50))
+    specs += [("mar", tuple(diseases[i::8])) for i in range(8)]
+    with ThreadPoolExecutor(8) as ex:
+        res = dict(ex.map(job, specs))
+    width = int(run("width", path, "mf").split()[1])
+    pr = res[("pr", evp)]
+    conds = [{"target": t, "value": 1, "log10Z": res[("pr", f)]["log10Z"], "Z": res[("pr", f)]["Z"],
+              "ref_uptime_ms": res[("pr", f)]["uptime_ms"]} for t, f in cond_files]
+    marg, mar_ms = {}, 0.0
+    for i in range(8):
+        txt = res[("mar", tuple(diseases[i::8]))]
+        for tag, f in parse_factors(txt).items():
+            marg[int(tag[1:])] = {"scope": f["scope"], "values": f["values"]}
+        mar_ms += parse_kv(txt)["uptime_ms"]
+    out = {"model": C4_MODEL, "evidence": C4_MODEL + ".evid", "heuristic": "mf", "ref_width": width,
+           "pr": {"Z": pr["Z"], "log10Z": pr["log10Z"], "ref_uptime_ms": pr["uptime_ms"]},
+           "conditioned": conds, "marginals": marg,
+           "ref_mar_ms_sum": mar_ms,
+           "note": "reference MAR timed per target in 8 parallel processes (sum of their uptimes); "
+                   "findings (ids 50..129) are evidence, their marginals are one-hot"}
+    with open(os.path.join(HERE, "config4_golden.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("config4", pr["log10Z"], width, len(marg), mar_ms)
+
+
+# CLI output parity (bn.cpp:224-258, mn.cpp:135-155, factor.cpp:291-321): the
+# exact stdout of the reference's own `bn` and `mn` binaries (oracle/_ref,
+# compiled from /root/reference/code) on the bundled models.  `bn` cases are
+# argv lists (run from tests/golden/models); `mn` cases are (argv, stdin).
+# Cases the reference crashes on (-mar with evidence and -mf/-wmf/-md,
+# SURVEY 0.6) are left out.
+CLI_BN = {
+    "bn_asia_pr": ["asia.uai", "-pr"],
+    "bn_asia_mar": ["asia.uai", "-mar"],
+    "bn_asia_pr_mar_mf": ["asia.uai", "-pr", "-mar", "-mf"],
+    "bn_asia_ev_pr_mar": ["asia.uai", "asia.uai.evid", "-pr", "-mar"],
+    "bn_asia_mar_sp": ["asia.uai", "-mar", "-sp"],
+    "bn_alarm_ev_pr_mf": ["alarm.uai", "alarm.uai.evid", "-pr", "-mf"],
+    "bn_alarm_ev_pr_mar": ["alarm.uai", "alarm.uai.evid", "-pr", "-mar"],
+    "bn_child_pr_mar_wmf": ["child.uai", "-pr", "-mar", "-wmf"],
+    "bn_hailfinder_ev_pr_md": ["hailfinder.uai", "hailfinder.uai.evid", "-pr", "-md"],
+    "bn_insurance_ve_mar_mf": ["insurance.uai", "-mar", "-ve", "-mf"],
+}
+CLI_MN = {
+    "mn_grid3x3_pr_mar": (["grid3x3.uai", "grid3x3-PR.uai.evid"], "PR\nMAR\nquit\n"),
+    "mn_grid3x3_mar_pr": (["grid3x3.uai", "grid3x3-MAR.uai.evid"], "MAR\npartition\nfoo\nquit\n"),
+}
+
+
+def cli_golden():
+    out_dir = os.path.join(HERE, "cli")
+    os.makedirs(out_dir, exist_ok=True)
+    ref = os.path.join(REPO, "oracle", "_ref")
+    cases = {}
+    for name, argv in CLI_BN.items():
+        r = subprocess.run([os.path.join(ref, "bn")] + argv, cwd=MODELS, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, (name, r.returncode)
+        cases[name] = {"tool": "bn", "argv": argv, "stdin": None, "stdout": r.stdout}
+    for name, (argv, stdin) in CLI_MN.items():
+        r = subprocess.run([os.path.join(ref, "mn")] + argv, cwd=MODELS, input=stdin, capture_output=True, text=True,
+                           timeout=600)
+        assert r.returncode == 0, (name, r.returncode)
+        cases[name] = {"tool": "mn", "argv": argv, "stdin": stdin, "stdout": r.stdout}
+    with open(os.path.join(HERE, "cli_golden.json"), "w") as f:
+        json.dump(cases, f, indent=1)
+    print("cli cases", len(cases))
+
+
+# BN::query_ve (model.cpp:204-248): the reference's own asia query file plus
+# random queries on alarm, each as the REPL's `query T | E` (bn.cpp:263, 347)
+QUERY_CASES = [("asia.uai", "asia.markov.query", "mf"), ("asia.uai", "asia.markov.query", "given"),
+               ("alarm.uai", "alarm.query", "mf")]
+
+
+def query_golden():
+    shutil.copyfile(os.path.join(REF_MODELS, "bayesnets", "asia.markov.query"), model_path("asia.markov.query"))
+    rng = random.Random(2024)
+    lines = []
+    for _ in range(12):
+        vs = rng.sample(range(37), rng.randint(1, 5))
+        nt = rng.randint(1, min(2, len(vs)))
+        t, e = vs[:nt], vs[nt:]
+        lines.append("query " + ", ".join(map(str, t)) + ((" | " + ", ".join(map(str, e))) if e else ""))
+    with open(model_path("alarm.query"), "w") as f:
+        f.write("\n".join(lines) + "\nquit\n")
+    cases = []
+    for model, qf, h in QUERY_CASES:
+        res = parse_factors(run("query", model_path(model), h, model_path(qf)))
+        queries = [l for l in open(model_path(qf)) if l.startswith("query ")]
+        cases.append({"model": model, "queries": qf, "heuristic": h, "lines": [q.strip() for q in queries],
+                      "results": [res["Q%d" % i] for i in range(len(queries))]})
+        print("query", model, qf, h, len(queries))
+    with open(os.path.join(HERE, "query_golden.json"), "w") as f:
+        json.dump({"cases": cases}, f, indent=1)
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["sp"]:
+    if sys.argv[1:] == ["query"]:
+        query_golden()
+    elif sys.argv[1:] == ["cli"]:
+        cli_golden()
+    elif sys.argv[1:] == ["config4"]:
+        config4_golden()
+    elif sys.argv[1:] == ["sp"]:
         sp_golden()
     elif sys.argv[1:] == ["corpus"]:
         corpus_golden()
@@ -345,3 +482,6 @@ if __name__ == "__main__":
         main()
         sp_golden()
         corpus_golden()
+        config4_golden()
+        cli_golden()
+        query_golden()

@@ -1,16 +1,18 @@
 """The C++ class mirror (include/bnpp/bn.hpp) and the bn/mn-compatible CLI
 (bin/bnpp): compile-and-link on CPU; run on the GPU against the reference's
 grid3x3 / network fixtures (models/markovnets/*.PR)."""
+import json
 import os
 import re
 import subprocess
 
 import pytest
 
-from conftest import REPO, model_path
+from conftest import GOLDEN, MODELS, REPO, model_path
 
 LIB = os.path.join(REPO, "bn-pp_amd", "lib")
 CLI = os.path.join(REPO, "bn-pp_amd", "bin", "bnpp")
+CLI_MN = os.path.join(REPO, "bn-pp_amd", "bin", "bnpp-mn")
 
 
 def _build_mirror_check(tmp_path):
@@ -21,8 +23,22 @@ def _build_mirror_check(tmp_path):
     return exe
 
 
+def _build_query_check(tmp_path):
+    exe = str(tmp_path / "query_check")
+    subprocess.run(["g++", "-std=c++17", "-O1", os.path.join(REPO, "tests", "cpp", "query_check.cpp"),
+                    "-I" + os.path.join(REPO, "include"), "-L" + LIB, "-lbnpp", "-Wl,-rpath," + LIB, "-o", exe],
+                   check=True, capture_output=True, timeout=300)
+    return exe
+
+
 def test_mirror_compiles_and_links(tmp_path):
     assert os.path.exists(_build_mirror_check(tmp_path))
+    assert os.path.exists(_build_query_check(tmp_path))
+
+
+def test_cli_binaries_built():
+    for exe in (CLI, CLI_MN):
+        assert os.access(exe, os.X_OK), exe
 
 
 @pytest.mark.gpu
@@ -69,3 +85,97 @@ def test_cli_sum_product_matches_reference(golden_sp):
     assert len(got) == len(want)
     for a, b in zip(got, want):
         assert abs(a - b) < 1e-6, (a, b)
+
+
+def _mask(text):
+    """the reference's own timing line is the only run-dependent output"""
+    return re.sub(r">> Executed in [^\n]*ms\.", ">> Executed in <t>ms.", text)
+
+
+@pytest.mark.gpu
+def test_cli_output_identical_to_reference():
+    """bin/bnpp and bin/bnpp-mn print byte for byte what the reference's `bn`
+    and `mn` print (tests/golden/cli_golden.json, captured from the reference
+    binaries built from /root/reference/code): Partition / Marginals lines,
+    Factor printing (factor.cpp:291-321) including the default float format of
+    the first partition before `fixed` turns sticky, width-0 factors for
+    evidence variables, the mn prompt (mn.cpp:96-155).  Only the
+    `>> Executed in` timings are masked."""
+    with open(os.path.join(GOLDEN, "cli_golden.json")) as f:
+        cases = json.load(f)
+    for name, c in cases.items():
+        exe = CLI if c["tool"] == "bn" else CLI_MN
+        r = subprocess.run([exe] + c["argv"], cwd=MODELS, input=c["stdin"], capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, (name, r.stderr)
+        assert _mask(r.stdout) == _mask(c["stdout"]), name
+
+
+def _canonical(scope, values, cards):
+    """table -> {assignment tuple in sorted-variable order: value}"""
+    order = sorted(range(len(scope)), key=lambda i: scope[i])
+    out, idx = {}, [0] * len(scope)
+    for v in values:
+        out[tuple(idx[i] for i in order)] = v
+        for d in range(len(scope) - 1, -1, -1):        # last variable fastest
+            idx[d] += 1
+            if idx[d] < cards[scope[d]]:
+                break
+            idx[d] = 0
+    return out
+
+
+@pytest.mark.gpu
+def test_query_ve_matches_reference(tmp_path):
+    """BN::query_ve (model.cpp:204-248) through the C++ mirror against the
+    reference's answers (tests/golden/query_golden.json: the reference's own
+    asia.markov.query and 12 random alarm queries).  Scope order follows the
+    reference's unordered_set iteration, so tables are compared after a
+    canonical permutation; values within 1e-12."""
+    import bnpp
+    exe = _build_query_check(tmp_path)
+    with open(os.path.join(GOLDEN, "query_golden.json")) as f:
+        cases = json.load(f)["cases"]
+    for case in cases:
+        cards = bnpp.Model.load(model_path(case["model"])).cards
+        r = subprocess.run([exe, model_path(case["model"]), model_path(case["queries"]), case["heuristic"]],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        got = [l for l in r.stdout.splitlines() if l.startswith("Q")]
+        assert len(got) == len(case["results"])
+        for line, ref in zip(got, case["results"]):
+            head, mid, vals = line.split("|")
+            h = head.split()
+            scope = [int(x) for x in h[2:2 + int(h[1])]]
+            values = [float(x) for x in vals.split()]
+            assert sorted(scope) == sorted(ref["scope"]), (case["model"], line)
+            a, b = _canonical(scope, values, cards), _canonical(ref["scope"], ref["values"], cards)
+            assert a.keys() == b.keys()
+            for k in a:
+                assert abs(a[k] - b[k]) <= 1e-12 * max(1.0, abs(b[k])), (case["model"], line, k, a[k], b[k])
+
+
+def _uai_numbers(path):
+    toks = open(path).read().split()
+    return toks[0], [float(t) for t in toks[1:]]
+
+
+@pytest.mark.gpu
+def test_cli_uai_result_files_match_reference_fixtures(tmp_path):
+    """`bnpp ... -uai base` writes UAI-competition result files; against the
+    reference's own models/markovnets/grid3x3.uai.{PR,MAR} (6 significant
+    digits), evidence variables one-hot (`2 0 1`)."""
+    base = str(tmp_path / "g")
+    _cli(model_path("grid3x3.uai"), model_path("grid3x3-MAR.uai.evid"), "-mar", "-mf", "-uai", base)
+    kind, got = _uai_numbers(base + ".MAR")
+    rkind, want = _uai_numbers(model_path("grid3x3.uai.MAR"))
+    assert kind == rkind == "MAR" and len(got) == len(want)
+    for a, b in zip(got, want):
+        assert abs(a - b) <= 5e-6 * max(1.0, abs(b)), (got, want)
+    lines = open(base + ".MAR").read().splitlines()
+    for v in (0, 3, 4):                                  # grid3x3-MAR.uai.evid = {0:1, 3:1, 4:1}
+        assert lines[3 + v] == "2 0 1"
+    _cli(model_path("grid3x3.uai"), model_path("grid3x3-PR.uai.evid"), "-pr", "-mf", "-uai", base)
+    kind, got = _uai_numbers(base + ".PR")
+    assert kind == "PR" and got[0] == 1 and abs(got[1] - 14.8899) < 1e-4
+    assert open(base + ".PR").read().split() == open(model_path("grid3x3.uai.PR")).read().split()

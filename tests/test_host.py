@@ -332,3 +332,18 @@ def test_plan_reduces_kept_tables_hierarchically():
             os.environ.pop(k, None)
     assert many[3] < plain[3], (many[3], plain[3])
     assert many[6] <= plain[6] * 1.01
+
+
+def test_plan_stats_saturate_on_infeasible_widths():
+    """A min-fill order on the 32x32 grid (width 48) and on a 24x24 4-state
+    Potts grid plans tables of 2^49 / 4^36 entries: sizes and byte counts
+    saturate (plan.hpp kSatMax) instead of overflowing; the first plan reads as
+    far beyond any device, the second fails cleanly with OOM instead of
+    planning descriptors for it (tools/sanitize_check.sh runs this under UBSan)."""
+    m = bnpp.Model.from_dict(synth.ising_grid(32, 32, seed=0))
+    st = bnpp.plan_stats(m, 0, {}, "mf", dtype=bnpp.F64)
+    assert st[4] >= 46 and st[1] > 1e15
+    p = bnpp.Model.from_dict(synth.potts_grid(24, 24, k=4, seed=0))       # width 35: 4^36 entries
+    with pytest.raises(bnpp.BnppError) as e:
+        bnpp.plan_stats(p, 0, {}, "mf", dtype=bnpp.F32)
+    assert e.value.status == bnpp.ERR_OOM

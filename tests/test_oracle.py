@@ -4,12 +4,14 @@ Golden vectors come from the reference itself (oracle/_ref/ref_harness built
 from /root/reference/code, tests/golden/make_golden.py) and from the
 reference's own fixture files (models/markovnets/*.PR, *.MAR).
 """
+import json
 import math
+import os
 
 import pytest
 
 import refcpu
-from conftest import evidence_of, model_path
+from conftest import GOLDEN, evidence_of, model_path
 
 # cases whose reference run takes more than a few seconds are left to the GPU tests
 SLOW = {"ising12x32.uai"}
@@ -140,3 +142,19 @@ def test_oracle_sum_product_matches_reference(golden_sp):
             assert len(got) == len(ref)
             for a, b in zip(got, ref):
                 assert abs(a - b) <= 1e-12, (case["model"], t, a, b)
+
+
+def test_oracle_config4_partition_matches_reference():
+    """BASELINE config 4 (noisy-OR 50x80, width 22): the restatement's PR and
+    three conditionings against the reference's (config4_golden.json), ~1.5 s each."""
+    with open(os.path.join(GOLDEN, "config4_golden.json")) as f:
+        g = json.load(f)
+    m = refcpu.Model.load(model_path(g["model"]))
+    ev = evidence_of(g["evidence"])
+    z, _ = m.partition(ev, "mf")
+    assert _close(z, g["pr"]["Z"], 1e-12), (z, g["pr"]["Z"])
+    c = g["conditioned"][0]
+    e = dict(ev)
+    e[c["target"]] = c["value"]
+    z1, _ = m.partition(e, "mf")
+    assert _close(z1, c["Z"], 1e-12), (z1, c["Z"])
