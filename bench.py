@@ -35,8 +35,8 @@ PR's factor-entries at the measured cpu_baseline rate.  "secondary": 10x10
 (reference-runnable): the reference's own BN::marginals (oracle/_ref
 ref_harness mar, one core, taskset) timed in this run, beside the GPU
 per-target and bucket-tree MAR, with the largest difference between them.
-"fp64_bucket": the k=4, w=13 bucket in the reference's precision (bit-exact
-path), with its own roofline fraction.
+"fp64_bucket": the same k=4, w=14 bucket in the reference's precision
+(bit-exact path; 17.2 GB per launch), with its own roofline fraction.
 """
 import argparse
 import json
@@ -203,7 +203,7 @@ def reference_bound(rec, cpu_rate):
                                   "factor-entries of the width-%d column-sweep PR / measured cpu_baseline rate" % rows})
 
 
-def fp64_bucket(ctx, dev, stream, rank, k=4, w=13, steps=10):
+def fp64_bucket(ctx, dev, stream, rank, k=4, w=14, steps=10):
     """The bench bucket in fp64 (the reference's arithmetic; bit-exact against
     it): m(x, S_1..S_w) * f(x, y) -> sum_x, timed with HIP events on the
     launch stream, with an exact spot check against the same sums in torch."""
