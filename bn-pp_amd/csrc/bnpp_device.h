@@ -126,8 +126,13 @@ __host__ __device__ constexpr int slab_key(int k, int c0, int v) { return 16384 
 //   kChainFwdS / kChainBwdS: the forward / backward layouts with the 2^F table
 //              of one rest entry split over 2^(F-4) waves (chainsplit.cuh;
 //              K = 2, fp32, F = 5..8), one workgroup per 64 rest entries
-enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2, kChainSum = 3, kChainFwdV = 4, kChainFwdS = 5, kChainBwdS = 6 };
-__host__ __device__ inline bool chain_split_form(int form) { return form == kChainFwdS || form == kChainBwdS; }
+//   kChainFwdSD / kChainBwdSD: the same with dense addressing (rest of <= 2
+//              dims, dim 0 a power of two, slots one dense block of strides)
+enum ChainForm : int32_t { kChainFwd = 1, kChainBwd = 2, kChainSum = 3, kChainFwdV = 4, kChainFwdS = 5, kChainBwdS = 6,
+                           kChainFwdSD = 7, kChainBwdSD = 8 };
+__host__ __device__ inline bool chain_split_form(int form) {
+    return form == kChainFwdS || form == kChainBwdS || form == kChainFwdSD || form == kChainBwdSD;
+}
 // Which slots G_j depends on besides its own (x_j, n_j): the next slot (j+1,
 // e.g. a forward sweep's vertical factor), the previous one (j-1, backward),
 // or any (every G value of a bucket fetched separately; small tables only).

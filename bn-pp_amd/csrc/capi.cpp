@@ -189,7 +189,7 @@ uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<i
     mix((uint64_t)part);
     mix((uint64_t)n_parts);
     // the planner's tuning knobs change the plan and its arena need
-    for (const char *k : {"BNPP_NO_SPLIT", "BNPP_SPLIT_MIN_F", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_NO_REDUCE_MANY",
+    for (const char *k : {"BNPP_NO_SPLIT", "BNPP_NO_DENSE", "BNPP_SPLIT_MIN_F", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_NO_REDUCE_MANY",
                           "BNPP_CHAIN_RUN_MAX", "BNPP_NO_CHAIN_FWDV", "BNPP_NO_STREAM", "BNPP_NO_SLAB", "BNPP_MAX_TILE"}) {
         const char *v = std::getenv(k);
         mix(0x9e37u);
@@ -391,7 +391,7 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     for (auto &bp : batches) {
         Schedule s;
         const double tb = now_ms();
-        if (!build_schedule(bp, d.cards, src_sizes, eb, max_vec_for(dtype), s, &msg))
+        if (!build_schedule(bp, d.cards, src_sizes, eb, max_vec_for(dtype), s, &msg, budget))
             return set_err(s.arena_bytes >= kSatMax ? BNPP_ERR_OOM : BNPP_ERR_INVALID, msg);
         if (timing) std::fprintf(stderr, "[bnpp] build_schedule call %.1f ms\n", now_ms() - tb);
         entries += s.entries;

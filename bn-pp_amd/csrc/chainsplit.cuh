@@ -26,6 +26,16 @@
 // two (forward) or one (backward) tiles' loads in flight while a tile is
 // computed (tools/chainbw.hip: the 8-bucket split access pattern moves 5.4-5.5
 // TB/s against 5.1-5.3 for 6-bucket runs one thread per rest entry).
+//
+// Dense runs (DENSE, forms kChainFwdSD / kChainBwdSD): the rest is at most two
+// dims, dim 0 a power of two contiguous on the streamed side, G_j constant
+// along it, and the slot strides one dense block (forward: x = slots as a
+// binary number times S; backward: the output slabs likewise).  That is every
+// run of a grid's column sweep.  There a tile's addresses are a uniform base
+// plus compile-time multiples of S plus the lane: no mixed-radix decode, no
+// per-slab 64-bit address arithmetic (tools/splitbw.hip: the same run with
+// constant addressing takes 5.99 / 5.81 ms per 2^32-entry message against the
+// general form's 6.90 / 6.58 ms).
 #pragma once
 #include "chain.cuh"
 
@@ -105,9 +115,13 @@ struct SplitState {
     int64_t is4[4], isw;          // input stride of slots 0-3; slots 4.. of this wave
     int64_t osl[4], osw;          // output stride of the 4 phase-2 local slots; the wave's other slots
     int32_t glds[F], gsj[F], gsq[F], gsn[F];
+    // dense runs: tiles per dim-0 row (log2), dim-1 strides (in, out, G_j), slab stride
+    int d_shift;
+    int64_t d_in1, d_out1, d_slab;
+    int32_t d_g1[F];
 };
 
-template <int F, int DEP>
+template <int F, int DEP, bool DENSE, int FORM>
 __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const BucketDesc &d, const int64_t *pool,
                                                  TableMeta *meta, int w) {
     constexpr int HB = 8 - F;
@@ -131,6 +145,16 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
         // below 4-HB carry the wave's digits (cgrp = w << HB | h, slot p = bit 3-p)
         if (p >= 4 - HB) c.osl[p - (4 - HB)] = os;
         else c.osw += (int64_t)((((w << HB) >> (3 - p)) & 1)) * os;
+    }
+    if constexpr (DENSE) {
+        c.d_shift = __builtin_ctz((uint32_t)((uint64_t)pool[0] & 0xffffffffu)) - 6;     // card0 / 64 tiles per row
+        const int64_t *r1 = pool + (4 + F);
+        const bool two = d.n_dims == 2;
+        c.d_in1 = two ? r1[2] : 0;
+        c.d_out1 = two ? r1[3] : 0;
+#pragma unroll
+        for (int j = 0; j < F; ++j) c.d_g1[j] = two ? (int32_t)r1[4 + j] : 0;
+        c.d_slab = FORM == kChainFwd ? sl[2 * (F - 1)] : sl[1];          // is[F-1] / os[0]
     }
     const int64_t *st = sl + 2 * F;
     int gi = 1;
@@ -171,7 +195,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Persistent workgroups walk the level's tiles (64 rest entries each) grid-
 // stride; the next tile's message loads are issued before the current tile is
 // computed, so HBM stays busy through the exchange barriers and the stores.
-template <int F, int FORM, int DEP>
+template <int F, int FORM, int DEP, bool DENSE>
 __global__ __launch_bounds__(64 * (1 << (F - 4))) __attribute__((amdgpu_waves_per_eu(BNPP_SPLIT_WAVES > 0 ? BNPP_SPLIT_WAVES : 1)))
 void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const int64_t *__restrict__ pool,
                         TableMeta *__restrict__ meta, int64_t total_vblocks) {
@@ -204,7 +228,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         cur = bi;
         cur_begin = d.vblk_begin;
         cur_end = bi + 1 < n_desc ? descs[bi + 1].vblk_begin : total_vblocks;
-        split_load_state<F, DEP>(c, d, pool + d.dim_off, meta, w);
+        split_load_state<F, DEP, DENSE, FORM>(c, d, pool + d.dim_off, meta, w);
         if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta);
         lds_barrier();                                     // the previous bucket's tables are no longer read
         // G_j packed: entry (o, q, n, x) at 8 o + 4 q + 2 n + x holds G_j[o + q
@@ -226,7 +250,27 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     // A tile's 64 entries are consecutive along rest dim 0 (planner: its card
     // is a multiple of 64), so the mixed-radix decode is done once per tile on
     // uniform values and each lane adds lane * (stride on dim 0).
+    // dense runs: the tile's uniform bases (tin, tout) and G offsets in closed form
+    int64_t tin = 0, tout = 0;
     auto decode = [&](int64_t vb, int64_t &in_off, int64_t &out_off, int32_t (&gb)[F]) {
+        if constexpr (DENSE) {
+            const int64_t rel = vb - cur_begin;
+            const int64_t d0 = (rel & ((int64_t(1) << c.d_shift) - 1)) * kSplitRows, d1 = rel >> c.d_shift;
+            if constexpr (FORM == kChainFwd) {
+                tin = c.in_base + d0 + d1 * c.d_in1;
+                tout = d0 * N + d1 * c.d_out1;
+                in_off = tin + lane;
+                out_off = tout + (int64_t)lane * N;
+            } else {
+                tin = c.in_base + d0 * N + d1 * c.d_in1;
+                tout = d0 + d1 * c.d_out1;
+                in_off = tin + (int64_t)lane * N;
+                out_off = tout + lane;
+            }
+#pragma unroll
+            for (int j = 0; j < F; ++j) gb[j] = (int32_t)d1 * c.d_g1[j];
+            return;
+        }
         const int64_t tid0 = (vb - cur_begin) * kSplitRows;
         const int row = 4 + F;
         const int64_t *dp = c.dims;
@@ -259,7 +303,27 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     };
     // the tile's message loads (16 values per lane)
     auto issue = [&](int64_t in_off, float (&rg)[16]) {
-        if constexpr (FORM == kChainFwd) {
+        if constexpr (DENSE && FORM == kChainFwd) {
+            // slab x = (slots 0-3 = e) << (F - 4) | (slots 4.. = w), at x * S
+            const T *wb = c.big + tin + (int64_t)w * c.d_slab + lane;
+            const int64_t step = c.d_slab << (F - 4);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                if constexpr (BNPP_SPLIT_NTL != 0) rg[e] = __builtin_nontemporal_load((const gbl_t<T> *)(wb + e * step));
+                else rg[e] = gload(wb + e * step);
+            }
+        } else if constexpr (DENSE) {
+            // 64 input rows of N contiguous values at tin + row * N
+            const T *big = c.big + tin;
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int q = it * 64 + lane;
+                const int rw = w * RPW + q / CPR, ch = q % CPR;
+                const vec_t<T, 4> v = vload<4, kNtLoad || BNPP_SPLIT_NTL != 0, true>(big + (int64_t)rw * N + 4 * ch);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) rg[4 * it + k] = v[k];
+            }
+        } else if constexpr (FORM == kChainFwd) {
             // slab of assignment (slots 0-3 = e, slots 4.. = w): uniform base + 32-bit lane offset
             const int64_t w0 = readfirstlane64(in_off);
             const uint32_t lob = (uint32_t)((in_off - w0) * 4);
@@ -381,7 +445,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             lds_barrier();
             // the 64 rows are one contiguous block of 64 * N entries (planner-checked):
             // wave w stores its 4 KiB share, 1 KiB per instruction
-            T *out = c.out + __shfl(out_off, 0, 64);
+            T *out = c.out + (DENSE ? tout : __shfl(out_off, 0, 64));
             // (tiles are whole: the planner requires rest dim 0 to be a multiple of 64)
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
@@ -392,7 +456,21 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             }
         } else {
             // slab stores: entry e has n-digits 0-3 = (w << HB | h), slots 4.. = sc
-            {
+            if constexpr (DENSE) {
+                // output slab of n-digits (slot p at S << p): e's local bits are
+                // slots 4-HB .. F-1 (MSB first), the wave's digits the others
+                int wsl = 0;
+#pragma unroll
+                for (int p = 0; p < 4 - HB; ++p) wsl |= (((w << HB) >> (3 - p)) & 1) << p;
+                T *wb = c.out + tout + (int64_t)wsl * c.d_slab + lane;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    int sl = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) sl |= ((e >> (3 - b)) & 1) << (4 - HB + b);
+                    store_n<T, 1, kNtStore, true>(wb + (int64_t)sl * c.d_slab, &t[e]);
+                }
+            } else {
                 const int64_t w0 = readfirstlane64(out_off);
                 const uint32_t lob = (uint32_t)((out_off - w0) * 4);
                 T *wb = c.out + w0 + c.osw;                // uniform
@@ -486,7 +564,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
 #ifndef BNPP_SPLIT_WAVES_PER_CU
 #define BNPP_SPLIT_WAVES_PER_CU 16     // resident waves per CU the persistent grid is sized for
 #endif
-template <int F, int FORM, int DEP>
+template <int F, int FORM, int DEP, bool DENSE>
 static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_t stream) {
     const size_t shm = kRedBytes + split_xch_bytes(F) + split_img_bytes(F) + (size_t)small_elems * sizeof(float);
     // per device (a process may drive several): the 160-KiB LDS opt-in of
@@ -504,7 +582,7 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     {
         std::lock_guard<std::mutex> g(ds.mu);
         if (!ds.done[dev]) {
-            ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP>,
+            ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP, DENSE>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (hipDeviceGetAttribute(&ds.cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
                 ds.cus[dev] <= 0)
@@ -516,16 +594,19 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     }
     const int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
     const int64_t grid = BNPP_SPLIT_FLAT ? a.vblocks : a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
-    hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP>), dim3((unsigned)grid), dim3(64 * split_waves(F)), shm,
+    hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP, DENSE>), dim3((unsigned)grid), dim3(64 * split_waves(F)), shm,
                        stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
     return hipGetLastError();
 }
 
-// forms kChainFwdS / kChainBwdS (bnpp_device.h), K = 2, F = 5..8, dep next / prev
-#define BNPP_CASE_CHAIN_SPLIT(F, FORM, KFORM, DEP) \
-    case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F: return go_chain_split<F, KFORM, DEP>(a, small_elems, stream);
-#define BNPP_CASE_CHAIN_SPLIT_OK(F, FORM, KFORM, DEP) case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F: return true;
-#define BNPP_CHAIN_SPLIT_FD(X, F) X(F, 5, kChainFwd, 0) X(F, 5, kChainFwd, 1) X(F, 6, kChainBwd, 0) X(F, 6, kChainBwd, 1)
+// forms kChainFwdS / kChainBwdS and their dense variants kChainFwdSD /
+// kChainBwdSD (bnpp_device.h), K = 2, F = 5..8, dep next / prev
+#define BNPP_CASE_CHAIN_SPLIT(F, FORM, KFORM, DEP, DENSE) \
+    case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F: return go_chain_split<F, KFORM, DEP, DENSE>(a, small_elems, stream);
+#define BNPP_CASE_CHAIN_SPLIT_OK(F, FORM, KFORM, DEP, DENSE) case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F: return true;
+#define BNPP_CHAIN_SPLIT_FD(X, F) X(F, 5, kChainFwd, 0, false) X(F, 5, kChainFwd, 1, false) \
+    X(F, 6, kChainBwd, 0, false) X(F, 6, kChainBwd, 1, false) X(F, 7, kChainFwd, 0, true) X(F, 7, kChainFwd, 1, true) \
+    X(F, 8, kChainBwd, 0, true) X(F, 8, kChainBwd, 1, true)
 #define BNPP_CHAIN_SPLIT(X) BNPP_CHAIN_SPLIT_FD(X, 5) BNPP_CHAIN_SPLIT_FD(X, 6) BNPP_CHAIN_SPLIT_FD(X, 7) \
     BNPP_CHAIN_SPLIT_FD(X, 8)
 

@@ -294,6 +294,20 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
             V = bv;
         }
     }
+    // dense addressing (chainsplit.cuh DENSE): rest of <= 2 dims, dim 0 a power
+    // of two contiguous on the streamed side, G constant along it, slot strides
+    // one dense block
+    if (form == kChainFwdS || form == kChainBwdS) {
+        const bool fw = form == kChainFwdS;
+        const char *nd = std::getenv("BNPP_NO_DENSE");
+        bool dense = !(nd && *nd == '1') && !md.empty() && md.size() <= 2 && md[0].card >= (uint64_t)kSplitRowsHost &&
+                     (md[0].card & (md[0].card - 1)) == 0 && (fw ? md[0].in == 1 : md[0].in == N);
+        for (int j = 0; dense && j < F; ++j) dense = md[0].g[j] == 0;
+        const int64_t S = fw ? is[F - 1] : os[0];
+        for (int p = 0; dense && p < F; ++p) dense = S > 0 && (fw ? is[p] : os[p]) == (S << (fw ? F - 1 - p : p));
+        const int dform = fw ? kChainFwdSD : kChainBwdSD;
+        if (dense && chain_supported(eb, chain_key(dform, K, F, dep))) form = dform;
+    }
     if (fwd_v && !std::getenv("BNPP_NO_CHAIN_FWDV") && chain_supported(eb, chain_key(kChainFwdV, K, F, dep))) {
         form = kChainFwdV;
         V = chain_fwd_v(N, eb);
@@ -317,7 +331,8 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         // the streamed side linear in the thread index: a wave spans 64 * V
         // consecutive rest entries -> uniform base + 32-bit lane byte offset
         bool lin = !md.empty();
-        const bool fwdf = form == kChainFwd || form == kChainFwdV || form == kChainSum || form == kChainFwdS;
+        const bool fwdf = form == kChainFwd || form == kChainFwdV || form == kChainSum || form == kChainFwdS ||
+                          form == kChainFwdSD;
         int64_t s0 = md.empty() ? 0 : (fwdf ? md[0].in : md[0].out);
         for (size_t q = 0; lin && q + 1 < md.size(); ++q) {
             const int64_t a = fwdf ? md[q].in : md[q].out, nb = fwdf ? md[q + 1].in : md[q + 1].out;
@@ -1601,7 +1616,7 @@ int64_t plan_arena_bytes(const VEPlan &p, int elem_bytes) {
 
 bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<int> &cards,
                     const std::vector<int64_t> &src_sizes, int elem_bytes, int max_vec, Schedule &s,
-                    std::string *msg) {
+                    std::string *msg, int64_t arena_cap) {
     s = Schedule{};
     const bool timing = std::getenv("BNPP_TIMING") != nullptr;
     auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -1625,13 +1640,107 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     }
     s.n_tables = (int)s.table_size.size();
     s.table_offset.resize(s.n_tables, -1);
-    auto remap = [&](size_t pi, int t) { return t < s.n_src ? t : msg_base[pi] + (t - s.n_src); };
+    // Many plans (per-target MAR, BN::marginals's one VE per target): a bucket
+    // structurally identical to one of an earlier plan -- the same summed
+    // variable, output layout, level and inputs (sources or identical buckets'
+    // outputs, with the same views) -- computes the same table bit for bit, so
+    // it runs once and every plan reads its output.  Targets whose min-fill
+    // orders share a prefix share those buckets (about half of the 12x32 grid's
+    // 147,456).  canon[t]: the table every later reference to t reads.
+    std::vector<int> canon(s.n_tables);
+    for (int t = 0; t < s.n_tables; ++t) canon[t] = t;
+    const char *nd = std::getenv("BNPP_NO_DEDUP");
+    const bool dedup = plans.size() > 1 && !(nd && *nd == '1');
+    if (dedup) {
+        struct Key {
+            uint64_t h1, h2;
+            int t;
+        };
+        std::vector<Key> keys(s.n_tables - s.n_src);
+        parallel_for((int64_t)plans.size(), [&](int64_t pi) {
+            const VEPlan &p = *plans[pi];
+            std::vector<std::pair<uint64_t, uint64_t>> th(p.msgs.size(), {0, 0});
+            for (const BucketSpec &b : p.buckets) {
+                uint64_t h1 = 0x9e3779b97f4a7c15ull, h2 = 0xc2b2ae3d27d4eb4full;
+                auto mix = [&](uint64_t x) {
+                    h1 = (h1 ^ x) * 0x100000001b3ull;
+                    h1 ^= h1 >> 29;
+                    h2 = (h2 + x + 0x632be59bd9b4e019ull) * 0x9e3779b97f4a7c15ull;
+                    h2 ^= h2 >> 31;
+                };
+                mix((uint64_t)(uint32_t)b.elim_var);
+                mix((uint64_t)b.level);
+                mix(b.divide ? 1 : 0);
+                mix(b.out_vars.size());
+                for (int v : b.out_vars) mix((uint64_t)v);
+                mix(b.chain_x.size() * 131 + b.chain_n.size() * 7 + (uint64_t)b.chain_gmask);
+                for (int v : b.chain_x) mix((uint64_t)(uint32_t)v);
+                for (int v : b.chain_n) mix((uint64_t)(uint32_t)v);
+                mix(p.cards_ext.size());
+                for (const View &v : b.in) {
+                    if (v.table < p.n_src) {
+                        mix(0xabcdull);
+                        mix((uint64_t)v.table);
+                    } else {
+                        mix(th[v.table - p.n_src].first);
+                        mix(th[v.table - p.n_src].second);
+                    }
+                    mix((uint64_t)v.base);
+                    for (size_t j = 0; j < v.vars.size(); ++j) {
+                        mix((uint64_t)v.vars[j]);
+                        mix((uint64_t)v.strides[j]);
+                    }
+                }
+                th[b.out_table - p.n_src] = {h1, h2};
+            }
+            for (size_t i = 0; i < p.msgs.size(); ++i) {
+                const int g = msg_base[pi] + (int)i;
+                keys[g - s.n_src] = {th[i].first, th[i].second, g};
+            }
+        });
+        std::sort(keys.begin(), keys.end(), [](const Key &a, const Key &b) {
+            return a.h1 != b.h1 ? a.h1 < b.h1 : a.h2 != b.h2 ? a.h2 < b.h2 : a.t < b.t;
+        });
+        for (size_t i = 1; i < keys.size(); ++i)
+            if (keys[i].h1 == keys[i - 1].h1 && keys[i].h2 == keys[i - 1].h2 && (keys[i].h1 | keys[i].h2) != 0)
+                canon[keys[i].t] = canon[keys[i - 1].t];      // the first occurrence (lowest id) of the group
+    }
+    auto remap = [&](size_t pi, int t) { return t < s.n_src ? t : canon[msg_base[pi] + (t - s.n_src)]; };
+    // a bucket runs when it produces its table's canonical copy
+    auto kept = [&](size_t pi, const BucketSpec &b) {
+        const int g = msg_base[pi] + (b.out_table - s.n_src);
+        return canon[g] == g;
+    };
+    if (dedup) {
+        // work actually scheduled: the kept buckets' factor-entries and traffic
+        // (plain buckets; a schedule with fused runs keeps the plans' sums)
+        double e = 0, mv = 0;
+        bool plain = true;
+        for (size_t pi = 0; pi < plans.size() && plain; ++pi) {
+            const std::vector<int> &pc = plans[pi]->cards_ext.empty() ? cards : plans[pi]->cards_ext;
+            for (const BucketSpec &b : plans[pi]->buckets) {
+                if (!b.chain_x.empty()) {
+                    plain = false;
+                    break;
+                }
+                if (!kept(pi, b)) continue;
+                e += (double)table_size(chain_scope(b.in), pc);
+                mv += (double)table_size(b.out_vars, pc);
+                for (const View &v : b.in) mv += (double)table_size(v.vars, pc);
+            }
+        }
+        if (plain) {
+            s.entries = e;
+            s.elems_moved = mv;
+        }
+    }
 
     // lifetimes: produced level, last consuming level
     const int kForever = INT_MAX;
     std::vector<int> born(s.n_tables, 0), last(s.n_tables, -1);
     for (size_t pi = 0; pi < plans.size(); ++pi) {
         for (const BucketSpec &b : plans[pi]->buckets) {
+            if (!kept(pi, b)) continue;
             born[remap(pi, b.out_table)] = b.level;
             for (const View &v : b.in) {
                 int t = remap(pi, v.table);
@@ -1653,20 +1762,70 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     }
     std::vector<std::vector<int>> born_at(n_levels + 2), dies_at(n_levels + 2);
     for (int t = s.n_src; t < s.n_tables; ++t) {
+        if (canon[t] != t) continue;                  // an alias: never placed
         born_at[born[t]].push_back(t);
         if (last[t] != kForever) dies_at[std::max(last[t], born[t])].push_back(t);
     }
     const double Tl = clk();
-    Arena arena;
-    for (int L = 1; L <= n_levels; ++L) {
-        for (int t : born_at[L]) s.table_offset[t] = arena.alloc(sat_mul(s.table_size[t], elem_bytes));
-        for (int t : dies_at[L]) arena.release(s.table_offset[t], sat_mul(s.table_size[t], elem_bytes));
+    // Many plans (per-target MAR): each plan's tables are placed in an arena
+    // of its own, in parallel, and the arenas laid side by side -- when their
+    // sum fits arena_cap.  One shared arena (below) reuses memory across plans
+    // and is the fallback; it is a serial best-fit walk over every table
+    // (136 ms for the 147,456 buckets of the 12x32 per-target MAR).
+    bool placed = false;
+    const char *sa = std::getenv("BNPP_SHARED_ARENA");
+    if (plans.size() > 1 && !(sa && *sa == '1')) {
+        std::vector<int64_t> tops(plans.size(), 0);
+        std::vector<char> sat(plans.size(), 0);
+        std::vector<int64_t> offs(s.n_tables, 0);
+        parallel_for((int64_t)plans.size(), [&](int64_t pi) {
+            const int t0 = msg_base[pi], t1 = t0 + (int)plans[pi]->msgs.size();
+            std::vector<std::vector<int>> ba(n_levels + 2), da(n_levels + 2);
+            for (int t = t0; t < t1; ++t) {
+                if (canon[t] != t) continue;
+                ba[born[t]].push_back(t);
+                if (last[t] != kForever) da[std::max(last[t], born[t])].push_back(t);
+            }
+            Arena a;
+            for (int L = 1; L <= n_levels; ++L) {
+                for (int t : ba[L]) offs[t] = a.alloc(sat_mul(s.table_size[t], elem_bytes));
+                for (int t : da[L]) a.release(offs[t], sat_mul(s.table_size[t], elem_bytes));
+            }
+            tops[pi] = a.top;
+            sat[pi] = a.saturated;
+        });
+        int64_t total = 0;
+        bool any_sat = false;
+        for (size_t pi = 0; pi < plans.size(); ++pi) {
+            total = sat_add(total, tops[pi]);
+            any_sat = any_sat || sat[pi];
+        }
+        if (!any_sat && total <= arena_cap) {
+            int64_t base = 0;
+            for (size_t pi = 0; pi < plans.size(); ++pi) {
+                const int t0 = msg_base[pi], t1 = t0 + (int)plans[pi]->msgs.size();
+                for (int t = t0; t < t1; ++t)
+                    if (canon[t] == t) s.table_offset[t] = base + offs[t];
+                base += tops[pi];
+            }
+            s.arena_bytes = total;
+            placed = true;
+        }
     }
-    s.arena_bytes = arena.top;
-    if (arena.saturated) {                   // tables of 2^58+ bytes: no descriptors for those
-        if (msg) *msg = "the plan's tables exceed any device (more than 2^58 bytes); use a narrower elimination order";
-        return false;
+    if (!placed) {
+        Arena arena;
+        for (int L = 1; L <= n_levels; ++L) {
+            for (int t : born_at[L]) s.table_offset[t] = arena.alloc(sat_mul(s.table_size[t], elem_bytes));
+            for (int t : dies_at[L]) arena.release(s.table_offset[t], sat_mul(s.table_size[t], elem_bytes));
+        }
+        s.arena_bytes = arena.top;
+        if (arena.saturated) {               // tables of 2^58+ bytes: no descriptors for those
+            if (msg) *msg = "the plan's tables exceed any device (more than 2^58 bytes); use a narrower elimination order";
+            return false;
+        }
     }
+    for (int t = s.n_src; t < s.n_tables; ++t)
+        if (canon[t] != t) s.table_offset[t] = s.table_offset[canon[t]];
     const double T1 = clk();
 
     // descriptors: built in parallel (one per bucket, private dims-pool rows),
@@ -1683,7 +1842,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     };
     std::vector<Item> items;
     for (size_t pi = 0; pi < plans.size(); ++pi)
-        for (const BucketSpec &b : plans[pi]->buckets) items.push_back(Item{b.level, pi, &b, BucketDesc{}, {}, 0, true, {}});
+        for (const BucketSpec &b : plans[pi]->buckets)
+            if (kept(pi, b)) items.push_back(Item{b.level, pi, &b, BucketDesc{}, {}, 0, true, {}});
     parallel_for((int64_t)items.size(), [&](int64_t idx) {
         Item &it = items[idx];
         BucketSpec b = *it.b;
@@ -1701,30 +1861,54 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
             if (msg) *msg = it.msg;
             return false;
         }
+    // order by (level, variant), ties by item index (stable), on compact keys
+    std::vector<std::pair<uint64_t, int>> sk(items.size());
+    for (size_t i = 0; i < items.size(); ++i)
+        sk[i] = {((uint64_t)(uint32_t)items[i].level << 32) | (uint32_t)items[i].key, (int)i};
+    std::sort(sk.begin(), sk.end());
     std::vector<int> ord(items.size());
-    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
-    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-        return items[a].level != items[b].level ? items[a].level < items[b].level : items[a].key < items[b].key;
+    std::vector<int64_t> pool_at(items.size() + 1, 0);
+    for (size_t i = 0; i < sk.size(); ++i) {
+        ord[i] = sk[i].second;
+        pool_at[i + 1] = pool_at[i] + (int64_t)items[ord[i]].pool.size();
+    }
+    s.pool.resize((size_t)pool_at.back());
+    s.descs.resize(items.size());
+    parallel_for((int64_t)ord.size(), [&](int64_t i) {
+        const Item &it = items[ord[i]];
+        std::copy(it.pool.begin(), it.pool.end(), s.pool.begin() + pool_at[i]);
+        s.descs[i] = it.d;
+        s.descs[i].dim_off = pool_at[i];
     });
-    size_t pool_total = 0;
-    for (const Item &it : items) pool_total += it.pool.size();
-    s.pool.reserve(pool_total);
-    s.descs.reserve(items.size());
     const bool dump = std::getenv("BNPP_DUMP_PLAN") != nullptr;
     for (size_t i = 0; i < ord.size();) {
         const Item &first = items[ord[i]];
-        Schedule::Group g{first.level, first.key, (int)s.descs.size(), 0, 0, 0};
+        Schedule::Group g{first.level, first.key, (int)i, 0, 0, 0};
         int64_t vb = 0;
         for (; i < ord.size() && items[ord[i]].level == g.level && items[ord[i]].key == g.variant; ++i) {
             const Item &it = items[ord[i]];
-            BucketDesc d = it.d;
-            d.dim_off = (int64_t)s.pool.size();
-            s.pool.insert(s.pool.end(), it.pool.begin(), it.pool.end());
+            BucketDesc &d = s.descs[i];
             d.vblk_begin = vb;
             const int64_t per_vb = d.chain && chain_split_form((d.chain >> 16) & 0xf) ? kSplitRowsHost : kBlock;
             vb += (d.n_tiles + per_vb - 1) / per_vb;
             g.small_elems = std::max(g.small_elems, d.big >= 0 || d.chain ? d.small_elems : 0);
-            if (dump) {
+            if (dump && d.chain) {
+                // chain run: per rest dim (card, in, out, G_j strides), then per slot (in, out)
+                const int F = d.chain & 0xff;
+                std::fprintf(stderr, "L%d chain F=%d form=%d dep=%d gmask=%x tiles=%lld base=%lld rest:", g.level, F,
+                             (d.chain >> 16) & 0xf, (d.chain >> 20) & 0xf, (d.chain >> 8) & 0xff, (long long)d.n_tiles,
+                             (long long)d.in_base[0]);
+                const int64_t *pl = it.pool.data();
+                for (int j = 0; j < d.n_dims; ++j, pl += 4 + F) {
+                    std::fprintf(stderr, " [%u:%lld,%lld|", (unsigned)((uint64_t)pl[0] & 0xffffffffu), (long long)pl[2],
+                                 (long long)pl[3]);
+                    for (int q = 0; q < F; ++q) std::fprintf(stderr, "%s%lld", q ? "," : "", (long long)pl[4 + q]);
+                    std::fprintf(stderr, "]");
+                }
+                std::fprintf(stderr, " slots:");
+                for (int q = 0; q < F; ++q) std::fprintf(stderr, " %lld/%lld", (long long)pl[2 * q], (long long)pl[2 * q + 1]);
+                std::fprintf(stderr, "\n");
+            } else if (dump) {
                 std::fprintf(stderr, "L%d n_in=%d k=%d tile=%dx%d big=%d bcls=%d tiles=%lld dims:", g.level, d.n_in, d.k,
                              d.v1, d.v2, d.big, d.big >= 0 ? d.bcls : 0, (long long)d.n_tiles);
                 for (int j = 0; j < d.n_dims; ++j) {
@@ -1739,9 +1923,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 for (int q = 0; q < d.n_in; ++q) std::fprintf(stderr, "%s%d", q ? "," : "", d.in_table[q]);
                 std::fprintf(stderr, "->%d\n", d.out_table);
             }
-            s.descs.push_back(d);
         }
-        g.end = (int)s.descs.size();
+        g.end = (int)i;
         g.vblocks = vb;
         s.groups.push_back(g);
     }

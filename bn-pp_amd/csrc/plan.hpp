@@ -1,8 +1,11 @@
 // Host-side planning for the fused bucket kernels (no HIP calls; unit-testable on CPU).
 #pragma once
 #include <cstdint>
+#include <climits>
 #include <functional>
 #include <string>
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "bnpp_device.h"
@@ -139,13 +142,34 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
 
 // Flattened, level-ordered launch schedule over one or more plans sharing the
 // same sources.  Tables: [0, n_src) sources, then every plan's messages.
+// vector allocator that default-initialises (no zero fill before the
+// parallel copy that fills a schedule's descriptor and pool arrays)
+template <typename T>
+struct DefaultInit : std::allocator<T> {
+    template <typename U>
+    struct rebind {
+        using other = DefaultInit<U>;
+    };
+    DefaultInit() = default;
+    template <typename U>
+    DefaultInit(const DefaultInit<U> &) noexcept {}
+    template <typename U>
+    void construct(U *p) noexcept {
+        ::new ((void *)p) U;
+    }
+    template <typename U, typename... A>
+    void construct(U *p, A &&...a) {
+        ::new ((void *)p) U(std::forward<A>(a)...);
+    }
+};
+
 struct Schedule {
     int n_src = 0;
     int n_tables = 0;
     std::vector<int64_t> table_size;        // entries, per table (sources included)
     std::vector<int64_t> table_offset;      // bytes into the arena (messages only; -1 for sources)
-    std::vector<BucketDesc> descs;          // grouped by level, vblk_begin relative to the level
-    std::vector<int64_t> pool;
+    std::vector<BucketDesc, DefaultInit<BucketDesc>> descs;   // grouped by level, vblk_begin relative to the level
+    std::vector<int64_t, DefaultInit<int64_t>> pool;
     struct Group {                          // one launch: buckets of one level and one kernel variant
         int level, variant, begin, end;
         int64_t vblocks;
@@ -168,8 +192,11 @@ int64_t plan_peak_bytes(const VEPlan &p, int elem_bytes);
 // best-fit allocator, so fragmentation included).
 int64_t plan_arena_bytes(const VEPlan &p, int elem_bytes);
 
+// arena_cap: the most device memory the schedule's arena may take; several
+// plans get arenas of their own (placed in parallel) when their sum fits it,
+// else one shared arena
 bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<int> &cards,
                     const std::vector<int64_t> &src_sizes, int elem_bytes, int max_vec, Schedule &s,
-                    std::string *msg);
+                    std::string *msg, int64_t arena_cap = INT64_MAX);
 
 }  // namespace bnpp

@@ -321,13 +321,15 @@ def test_split_runs_identical_to_unfused(ctx, capfd, spec):
     """Binary fp32 sweeps tall enough for the split chain form (chainsplit.cuh:
     runs of 5..8 buckets, the 2^F table of a rest entry over 2^(F-4) waves):
     partition and tree marginals bit-identical to the one-thread runs of <= 6
-    buckets and to one bucket per launch; the plan holds split runs (forms 5, 6)."""
+    buckets and to one bucket per launch; the plan holds split runs with dense
+    addressing (forms 7, 8) and, with BNPP_NO_DENSE, with the general one
+    (forms 5, 6) -- both bit-identical."""
     r, c, ev = spec
     ev = ev or {}
     m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=13))
     col = [i * c + j for j in range(c) for i in range(r)]
-    knobs = [{"BNPP_DEBUG_CHAIN": "1"}, {"BNPP_SPLIT_MIN_F": "7"}, {"BNPP_NO_SPLIT": "1"},
-             {"BNPP_NO_SPLIT": "1", "BNPP_CHAIN_RUN_MAX": "6"}, {"BNPP_NO_CHAIN": "1"}]
+    knobs = [{"BNPP_DEBUG_CHAIN": "1"}, {"BNPP_DEBUG_CHAIN": "1", "BNPP_NO_DENSE": "1"}, {"BNPP_SPLIT_MIN_F": "7"},
+             {"BNPP_NO_SPLIT": "1"}, {"BNPP_NO_SPLIT": "1", "BNPP_CHAIN_RUN_MAX": "6"}, {"BNPP_NO_CHAIN": "1"}]
     res = []
     for kn in knobs:
         os.environ.update(kn)
@@ -344,7 +346,8 @@ def test_split_runs_identical_to_unfused(ctx, capfd, spec):
                 del os.environ[key]
         if "BNPP_DEBUG_CHAIN" in kn:
             err = capfd.readouterr().err
-            assert "run form 5 K=2 F=8" in err or "run form 6 K=2 F=8" in err, err[-2000:]
+            forms = (5, 6) if "BNPP_NO_DENSE" in kn else (7, 8)
+            assert any("run form %d K=2 F=8" % f in err for f in forms), err[-2000:]
     for out in res[1:]:
         assert out == res[0]
     want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
@@ -404,3 +407,42 @@ def test_split_runs_of_two_components_share_launches(ctx, capfd):
     ma, mb = bnpp.Model.from_dict(a), bnpp.Model.from_dict(b)
     want = bnpp.partition(ctx, ma, {}, "mf", bnpp.F64, order=col)[0] + bnpp.partition(ctx, mb, {}, "mf", bnpp.F64, order=col)[0]
     assert abs(res[0] - want) <= 1e-6 * abs(want), (res[0], want)
+
+
+@pytest.mark.parametrize("rows,cols,hop", [(12, 6, 3), (10, 5, 2)])
+def test_runs_with_non_neighbour_g_fall_back_safely(ctx, rows, cols, hop):
+    """A column sweep whose buckets also hold a factor to the variable `hop`
+    rows below (G_j depends on slot j + hop, not a neighbouring one: ChainDep
+    any).  Such runs cannot use the split forms; the planner falls back to the
+    one-thread forms only where their own layout conditions hold (ADVICE r2:
+    a backward fallback once skipped them), else to shorter runs.  Partition
+    and tree marginals bit-identical across the chain variants, and within
+    tolerance of the oracle's fp64 partition."""
+    import random
+    d = synth.ising_grid(rows, cols, seed=31)
+    rng = random.Random(5)
+    for c in range(cols):
+        for r in range(rows - hop):
+            j = rng.uniform(-0.5, 0.5)
+            e, ne = round(math.exp(j), 6), round(math.exp(-j), 6)
+            d["scopes"].append([r * cols + c, (r + hop) * cols + c])
+            d["values"].append([e, ne, ne, e])
+    m = bnpp.Model.from_dict(d)
+    col = [i * cols + j for j in range(cols) for i in range(rows)]
+    knobs = [{}, {"BNPP_NO_SPLIT": "1"}, {"BNPP_NO_DENSE": "1"}, {"BNPP_CHAIN_RUN_MAX": "5"}, {"BNPP_NO_CHAIN": "1"}]
+    res = []
+    for kn in knobs:
+        os.environ.update(kn)
+        os.environ["BNPP_TREE_SLOTS"] = "3"
+        try:
+            res.append([bnpp.partition(ctx, m, {}, "mf", dt, order=col)[0] for dt in (bnpp.F64, bnpp.F32)] +
+                       [bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F32, order=col)[0]])
+        finally:
+            for key in list(kn) + ["BNPP_TREE_SLOTS"]:
+                del os.environ[key]
+    for out in res[1:]:
+        assert out == res[0]
+    assert abs(res[0][1] - res[0][0]) <= 1e-6 * abs(res[0][0])
+    want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    for t in range(m.n_vars):
+        assert _close(res[0][2][t], want[t], 1e-5), (t, res[0][2][t], want[t])

@@ -112,7 +112,24 @@ def test_plan_stats():
     assert width == w == 13
     assert buckets >= 99 and levels >= 1 and entries > 0 and arena > 0
     st_mar = bnpp.plan_stats(m, 1, {}, "mf")
-    assert st_mar[3] > 50 * buckets          # one VE per target, batched
+    assert st_mar[3] > 10 * buckets          # one VE per target, batched, shared buckets once
+    os.environ["BNPP_NO_DEDUP"] = "1"
+    try:
+        st_all = bnpp.plan_stats(m, 1, {}, "mf")
+    finally:
+        del os.environ["BNPP_NO_DEDUP"]
+    assert st_all[3] > 50 * buckets          # every target's own copy of every bucket
+    assert st_all[3] > 2 * st_mar[3] and st_all[0] > st_mar[0]
+
+
+def test_per_target_plans_share_identical_buckets():
+    """BN::marginals runs one VE per target (model.cpp:326-334); targets whose
+    min-fill orders share a prefix share those buckets exactly (same inputs,
+    same layout, same level), so the schedule runs each once: 147,456 buckets
+    -> about 25,000 on the 12x32 strip, same result tables per target."""
+    m = bnpp.Model.load(model_path("ising12x32.uai"))
+    st = bnpp.plan_stats(m, 1, {}, "mf")
+    assert st[3] < 0.25 * 384 * 384
 
 
 def test_bad_arguments_are_rejected():
@@ -270,7 +287,9 @@ def test_plan_short_forward_runs_use_vector_form(capfd):
 def test_plan_forward_runs_of_six(capfd):
     """Binary fp32 sweeps of a checkpointed bucket tree fuse 6 forward buckets
     per pass (256-B rows staged in 128-B parts) and 6 backward ones in the
-    one-thread forms; with the split forms (chainsplit.cuh) runs of 7-8."""
+    one-thread forms; with the split forms (chainsplit.cuh) runs of 7-8 --
+    dense addressing (forms 7, 8) on a grid sweep, the general one (5, 6) with
+    BNPP_NO_DENSE."""
     from bnpp import synth
     m = bnpp.Model.from_dict(synth.ising_grid(16, 5, seed=11))
     col = [i * 5 + j for j in range(5) for i in range(16)]
@@ -279,8 +298,10 @@ def test_plan_forward_runs_of_six(capfd):
     m = bnpp.Model.from_dict(synth.ising_grid(18, 5, seed=11))
     col = [i * 5 + j for j in range(5) for i in range(18)]
     forms = _chain_forms(capfd, m, col, {"BNPP_TREE_SLOTS": "3"}, kind=3)
-    assert (5, 8) in forms and (6, 8) in forms, forms
+    assert (7, 8) in forms and (8, 8) in forms, forms
     assert max(f for _, f in forms) == 8
+    forms = _chain_forms(capfd, m, col, {"BNPP_TREE_SLOTS": "3", "BNPP_NO_DENSE": "1"}, kind=3)
+    assert (5, 8) in forms and (6, 8) in forms, forms
 
 
 def test_checkpoint_slot_memo_matches_fresh_search():
