@@ -16,6 +16,7 @@
 #include <new>
 #include <string>
 #include <utility>
+#include <thread>
 #include <vector>
 
 #include "model_io.hpp"
@@ -419,9 +420,16 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     stats[6] = moved * eb;
     stats[7] = (double)out.size();
     // the plans hold millions of small vectors (per-target MAR: one plan per
-    // target); free them on the worker threads instead of one by one here
+    // target, ~25 ms to free): a background thread frees them while the call
+    // goes on to upload and launch (plans of one bucket tree: here)
     const double tf = now_ms();
-    parallel_for((int64_t)plans.size(), [&](int64_t i) { VEPlan dead = std::move(plans[i]); });
+    if (plans.size() > 1) {
+        std::thread([dead = std::move(plans)]() mutable {
+            parallel_for((int64_t)dead.size(), [&](int64_t i) { VEPlan d = std::move(dead[i]); });
+        }).detach();
+    } else {
+        plans.clear();
+    }
     if (timing) std::fprintf(stderr, "[bnpp] plans freed in %.1f ms\n", now_ms() - tf);
     return BNPP_OK;
 }
@@ -487,8 +495,12 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
 void destroy_job(bnpp_job *job) {
     if (!job) return;
     (void)hipSetDevice(job->ctx->c.device);
-    free_program(job->pg);
-    free_sources(job->src);
+    // the buffers go back to the context's cache for the next call: nothing
+    // may still run on them (a job may have been launched on any stream; a
+    // hipFree would wait the same way)
+    (void)hipDeviceSynchronize();
+    free_program(job->ctx->c, job->pg);
+    free_sources(job->ctx->c, job->src);
     delete job;
 }
 
@@ -606,6 +618,7 @@ int bnpp_ctx_destroy(bnpp_ctx *ctx) {
     (void)hipSetDevice(ctx->c.device);
     if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
     drop_arena_cache(ctx->c);
+    drop_buffer_cache(ctx->c);
     delete ctx;
     return BNPP_OK;
 }

@@ -25,6 +25,27 @@ hipError_t dispatch_slab_single_f64(int key, const SingleArgs &a, hipStream_t st
 hipError_t dispatch_slab_level_f32(int key, const LevelArgs &a, hipStream_t stream);
 hipError_t dispatch_slab_level_f64(int key, const LevelArgs &a, hipStream_t stream);
 
+// Result tables out of the arena, one workgroup per table: 16-B moves while
+// both ends allow them (tables are 256-B aligned in the arena and the results
+// buffer), 4-B ones for the tail (sizes are whole fp32 / fp64 entries).
+__global__ __launch_bounds__(256) void copy_tables_kernel(const CopyItem *__restrict__ items, int n) {
+    const CopyItem c = items[blockIdx.x];
+    const int64_t n16 = c.bytes / 16;
+    const uint4 *s16 = static_cast<const uint4 *>(c.src);
+    uint4 *d16 = static_cast<uint4 *>(c.dst);
+    for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) d16[i] = s16[i];
+    const uint32_t *s4 = static_cast<const uint32_t *>(c.src);
+    uint32_t *d4 = static_cast<uint32_t *>(c.dst);
+    for (int64_t i = n16 * 4 + threadIdx.x; i < c.bytes / 4; i += blockDim.x) d4[i] = s4[i];
+    (void)n;
+}
+
+hipError_t launch_copies(const CopyItem *items, int n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(copy_tables_kernel, dim3((unsigned)n), dim3(256), 0, stream, items, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream) {
     if (a.d.n_tiles <= 0) return hipSuccess;
     if (a.d.big >= 0 && a.d.bcls == kBigSlab) {

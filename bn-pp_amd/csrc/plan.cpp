@@ -1698,12 +1698,19 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 keys[g - s.n_src] = {th[i].first, th[i].second, g};
             }
         });
-        std::sort(keys.begin(), keys.end(), [](const Key &a, const Key &b) {
-            return a.h1 != b.h1 ? a.h1 < b.h1 : a.h2 != b.h2 ? a.h2 < b.h2 : a.t < b.t;
+        // equal keys share their top bits: 64 shards sorted and grouped in parallel
+        constexpr int kShards = 64;
+        std::vector<std::vector<Key>> shard(kShards);
+        for (const Key &k : keys) shard[k.h1 >> 58].push_back(k);
+        parallel_for(kShards, [&](int64_t sh) {
+            std::vector<Key> &v = shard[sh];
+            std::sort(v.begin(), v.end(), [](const Key &a, const Key &b) {
+                return a.h1 != b.h1 ? a.h1 < b.h1 : a.h2 != b.h2 ? a.h2 < b.h2 : a.t < b.t;
+            });
+            for (size_t i = 1; i < v.size(); ++i)
+                if (v[i].h1 == v[i - 1].h1 && v[i].h2 == v[i - 1].h2 && (v[i].h1 | v[i].h2) != 0)
+                    canon[v[i].t] = canon[v[i - 1].t];  // the first occurrence (lowest id) of the group
         });
-        for (size_t i = 1; i < keys.size(); ++i)
-            if (keys[i].h1 == keys[i - 1].h1 && keys[i].h2 == keys[i - 1].h2 && (keys[i].h1 | keys[i].h2) != 0)
-                canon[keys[i].t] = canon[keys[i - 1].t];      // the first occurrence (lowest id) of the group
     }
     auto remap = [&](size_t pi, int t) { return t < s.n_src ? t : canon[msg_base[pi] + (t - s.n_src)]; };
     // a bucket runs when it produces its table's canonical copy

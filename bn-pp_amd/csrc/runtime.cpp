@@ -22,6 +22,51 @@ uint64_t bits_of(T x) {
 
 }  // namespace
 
+hipError_t get_buffer(Context &ctx, size_t bytes, void **p, size_t *cap) {
+    bytes = bytes ? bytes : 256;
+    {
+        std::lock_guard<std::mutex> g(ctx.buf_mu);
+        size_t best = ctx.buf_free.size();
+        for (size_t i = 0; i < ctx.buf_free.size(); ++i) {
+            const size_t c = ctx.buf_free[i].second;
+            if (c >= bytes && c <= 4 * bytes + 65536 && (best == ctx.buf_free.size() || c < ctx.buf_free[best].second))
+                best = i;
+        }
+        if (best < ctx.buf_free.size()) {
+            *p = ctx.buf_free[best].first;
+            *cap = ctx.buf_free[best].second;
+            ctx.buf_free_bytes -= *cap;
+            ctx.buf_free.erase(ctx.buf_free.begin() + best);
+            return hipSuccess;
+        }
+    }
+    const size_t c = (bytes + 65535) & ~(size_t)65535;       // 64-KiB granules: fewer distinct sizes
+    hipError_t e = hipMalloc(p, c);
+    *cap = e == hipSuccess ? c : 0;
+    return e;
+}
+
+void put_buffer(Context &ctx, void *p, size_t cap) {
+    if (!p) return;
+    constexpr size_t kMaxCached = (size_t)1 << 30, kMaxCount = 64;
+    {
+        std::lock_guard<std::mutex> g(ctx.buf_mu);
+        if (cap > 0 && ctx.buf_free_bytes + cap <= kMaxCached && ctx.buf_free.size() < kMaxCount) {
+            ctx.buf_free.push_back({p, cap});
+            ctx.buf_free_bytes += cap;
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+
+void drop_buffer_cache(Context &ctx) {
+    std::lock_guard<std::mutex> g(ctx.buf_mu);
+    for (auto &b : ctx.buf_free) (void)hipFree(b.first);
+    ctx.buf_free.clear();
+    ctx.buf_free_bytes = 0;
+}
+
 int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out) {
     const size_t eb = dt == kF32 ? 4 : 8;
     out = DeviceSources{};
@@ -60,7 +105,7 @@ int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values,
     }
     hipError_t err = hipSetDevice(ctx.device);
     if (err != hipSuccess) return fail(ctx, err, "hipSetDevice");
-    err = hipMalloc(&out.buf, host.size());
+    err = get_buffer(ctx, host.size(), &out.buf, &out.buf_cap);
     if (err != hipSuccess) return fail(ctx, err, "hipMalloc(sources)");
     err = hipMemcpy(out.buf, host.data(), host.size(), hipMemcpyHostToDevice);
     if (err != hipSuccess) return fail(ctx, err, "hipMemcpy(sources)");
@@ -68,8 +113,8 @@ int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values,
     return 0;
 }
 
-void free_sources(DeviceSources &s) {
-    if (s.buf) (void)hipFree(s.buf);
+void free_sources(Context &ctx, DeviceSources &s) {
+    put_buffer(ctx, s.buf, s.buf_cap);
     s = DeviceSources{};
 }
 
@@ -105,12 +150,17 @@ int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Execut
         }
     }
     const size_t mb = sizeof(TableMeta) * (size_t)sc.n_tables;
-    if ((err = hipMalloc(&ex.d_meta, mb + 16)) != hipSuccess) return fail(ctx, err, "hipMalloc(meta)");
-    if ((err = hipMalloc(&ex.d_meta0, mb + 16)) != hipSuccess) return fail(ctx, err, "hipMalloc(meta0)");
-    if ((err = hipMalloc(&ex.d_desc, sizeof(BucketDesc) * sc.descs.size() + 16)) != hipSuccess)
+    void *pm = nullptr, *pm0 = nullptr, *pd = nullptr, *pp = nullptr;
+    if ((err = get_buffer(ctx, mb + 16, &pm, &ex.cap_meta)) != hipSuccess) return fail(ctx, err, "hipMalloc(meta)");
+    ex.d_meta = static_cast<TableMeta *>(pm);
+    if ((err = get_buffer(ctx, mb + 16, &pm0, &ex.cap_meta0)) != hipSuccess) return fail(ctx, err, "hipMalloc(meta0)");
+    ex.d_meta0 = static_cast<TableMeta *>(pm0);
+    if ((err = get_buffer(ctx, sizeof(BucketDesc) * sc.descs.size() + 16, &pd, &ex.cap_desc)) != hipSuccess)
         return fail(ctx, err, "hipMalloc(desc)");
-    if ((err = hipMalloc(&ex.d_pool, sizeof(int64_t) * sc.pool.size() + 16)) != hipSuccess)
+    ex.d_desc = static_cast<BucketDesc *>(pd);
+    if ((err = get_buffer(ctx, sizeof(int64_t) * sc.pool.size() + 16, &pp, &ex.cap_pool)) != hipSuccess)
         return fail(ctx, err, "hipMalloc(pool)");
+    ex.d_pool = static_cast<int64_t *>(pp);
     if (mb && (err = hipMemcpy(ex.d_meta0, ex.h_meta.data(), mb, hipMemcpyHostToDevice)) != hipSuccess)
         return fail(ctx, err, "hipMemcpy(meta)");
     if (!sc.descs.empty() && (err = hipMemcpy(ex.d_desc, sc.descs.data(), sizeof(BucketDesc) * sc.descs.size(),
@@ -171,12 +221,13 @@ int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<
     return 0;
 }
 
-void free_executable(Executable &ex) {
+void free_executable(Context &ctx, Executable &ex) {
     if (ex.arena && ex.own_arena) (void)hipFree(ex.arena);
-    if (ex.d_meta) (void)hipFree(ex.d_meta);
-    if (ex.d_meta0) (void)hipFree(ex.d_meta0);
-    if (ex.d_desc) (void)hipFree(ex.d_desc);
-    if (ex.d_pool) (void)hipFree(ex.d_pool);
+    put_buffer(ctx, ex.d_meta, ex.cap_meta);
+    put_buffer(ctx, ex.d_meta0, ex.cap_meta0);
+    put_buffer(ctx, ex.d_desc, ex.cap_desc);
+    put_buffer(ctx, ex.d_pool, ex.cap_pool);
+    put_buffer(ctx, ex.d_copies, ex.cap_copies);
     ex = Executable{};
 }
 
@@ -222,29 +273,46 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
         pg.res_off.push_back(off);
         pg.res_size.push_back(sz);
     }
-    if ((err = hipMalloc(&pg.results, pg.results_bytes > 0 ? (size_t)pg.results_bytes : 256)) != hipSuccess)
+    if ((err = get_buffer(ctx, pg.results_bytes > 0 ? (size_t)pg.results_bytes : 256, &pg.results, &pg.results_cap)) !=
+        hipSuccess)
         return fail(ctx, err, "hipMalloc(results)");
     pg.parts.resize(batches.size());
     for (size_t b = 0; b < batches.size(); ++b) {
         int rc = make_executable(ctx, src, std::move(batches[b]), pg.parts[b], pg.arena);
         if (rc) return rc;
+        // the part's result tables, copied into `results` by one launch after it runs
+        Executable &ex = pg.parts[b];
+        std::vector<CopyItem> cp;
+        for (size_t p = 0; p < ex.sched.plan_result_table.size(); ++p) {
+            const int t = ex.sched.plan_result_table[p];
+            if (t < 0) continue;
+            cp.push_back({ex.h_meta[t].ptr, static_cast<unsigned char *>(pg.results) + pg.res_off[b][p],
+                          ex.sched.table_size[t] * eb});
+        }
+        ex.n_copies = (int)cp.size();
+        if (!cp.empty()) {
+            void *pc = nullptr;
+            if ((err = get_buffer(ctx, sizeof(CopyItem) * cp.size(), &pc, &ex.cap_copies)) != hipSuccess)
+                return fail(ctx, err, "hipMalloc(copies)");
+            ex.d_copies = static_cast<CopyItem *>(pc);
+            if ((err = hipMemcpy(ex.d_copies, cp.data(), sizeof(CopyItem) * cp.size(), hipMemcpyHostToDevice)) !=
+                hipSuccess)
+                return fail(ctx, err, "hipMemcpy(copies)");
+        }
     }
     return 0;
 }
 
 int launch_program(Context &ctx, Program &pg, hipStream_t stream) {
     const int64_t eb = pg.dtype == kF32 ? 4 : 8;
+    (void)eb;
     for (size_t b = 0; b < pg.parts.size(); ++b) {
         Executable &ex = pg.parts[b];
         int rc = launch(ctx, ex, stream);
         if (rc) return rc;
-        for (size_t p = 0; p < ex.sched.plan_result_table.size(); ++p) {
-            int t = ex.sched.plan_result_table[p];
-            if (t < 0) continue;
-            hipError_t err = hipMemcpyAsync(static_cast<unsigned char *>(pg.results) + pg.res_off[b][p],
-                                            ex.h_meta[t].ptr, (size_t)(ex.sched.table_size[t] * eb),
-                                            hipMemcpyDeviceToDevice, stream);
-            if (err != hipSuccess) return fail(ctx, err, "hipMemcpyAsync(result)");
+        if (ex.n_copies > 0) {
+            hipError_t err = launch_copies(ex.d_copies, ex.n_copies, stream);
+            if (err != hipSuccess) return fail(ctx, err, "launch_copies");
         }
     }
     return 0;
@@ -292,10 +360,10 @@ int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std
     return 0;
 }
 
-void free_program(Program &pg) {
-    for (Executable &ex : pg.parts) free_executable(ex);
+void free_program(Context &ctx, Program &pg) {
+    for (Executable &ex : pg.parts) free_executable(ctx, ex);
     if (pg.arena && !pg.arena_cached) (void)hipFree(pg.arena);
-    if (pg.results) (void)hipFree(pg.results);
+    put_buffer(ctx, pg.results, pg.results_cap);
     pg = Program{};
 }
 

@@ -3,7 +3,9 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "bnpp_device.h"
@@ -43,15 +45,35 @@ struct Context {
     // allocator the context holds on to it until it is destroyed
     void *arena_cache = nullptr;
     int64_t arena_cache_bytes = 0;
+    // small device buffers (sources, descriptors, dims pool, metadata, results)
+    // kept for reuse: a one-shot call otherwise pays ~10 hipMalloc / hipFree
+    // pairs (hipFree synchronises), several ms of a small model's PR
+    std::mutex buf_mu;
+    std::vector<std::pair<void *, size_t>> buf_free;   // (buffer, capacity)
+    size_t buf_free_bytes = 0;
 };
+
+// a device buffer of at least `bytes` from the context's cache (or hipMalloc);
+// `cap` receives its capacity, to hand back with put_buffer
+hipError_t get_buffer(Context &ctx, size_t bytes, void **p, size_t *cap);
+void put_buffer(Context &ctx, void *p, size_t cap);
+void drop_buffer_cache(Context &ctx);
 
 // Sources uploaded for one dtype: one device buffer, each factor pre-scaled by
 // an exact power of two so its max lies in [0.5, 1).
 struct DeviceSources {
     DType dtype = kF64;
     void *buf = nullptr;
+    size_t buf_cap = 0;
     std::vector<TableMeta> meta;
     std::vector<int64_t> size;
+};
+
+// one result table copied out of the arena (launch_copies: one launch for all)
+struct CopyItem {
+    const void *src;
+    void *dst;
+    int64_t bytes;
 };
 
 // A schedule bound to device buffers, launchable many times.
@@ -65,6 +87,9 @@ struct Executable {
     BucketDesc *d_desc = nullptr;
     int64_t *d_pool = nullptr;
     std::vector<TableMeta> h_meta;
+    CopyItem *d_copies = nullptr;       // result tables -> the program's results buffer
+    int n_copies = 0;
+    size_t cap_meta = 0, cap_meta0 = 0, cap_desc = 0, cap_pool = 0, cap_copies = 0;   // buffer capacities
 };
 
 // Several schedules (target batches of one MAR job) run back to back in one
@@ -77,28 +102,31 @@ struct Program {
     int64_t arena_bytes = 0;
     bool arena_cached = false;          // arena is the context's cache (not freed with the program)
     void *results = nullptr;
+    size_t results_cap = 0;
     int64_t results_bytes = 0;
     std::vector<std::vector<int64_t>> res_off;    // per part, per plan: byte offset (-1: constant 1)
     std::vector<std::vector<int64_t>> res_size;   // per part, per plan: entries
 };
 
 int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out);
-void free_sources(DeviceSources &s);
+void free_sources(Context &ctx, DeviceSources &s);
 int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex, void *shared_arena = nullptr);
 int launch(Context &ctx, Executable &ex, hipStream_t stream);
 // waits for `stream`, downloads result tables: values as stored (double) and the exp2 scale
 int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<std::vector<double>> &vals,
                   std::vector<int64_t> &exp2);
-void free_executable(Executable &ex);
+void free_executable(Context &ctx, Executable &ex);
 
 int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg,
                  bool use_cache = false);
+// copy n result tables (device array of CopyItem) in one launch (launch.hip)
+hipError_t launch_copies(const CopyItem *items, int n, hipStream_t stream);
 // release the context's cached arena
 void drop_arena_cache(Context &ctx);
 int launch_program(Context &ctx, Program &pg, hipStream_t stream);
 // result values (as stored, double) and exp2 of every plan, batches in order
 int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std::vector<double>> &vals,
                   std::vector<int64_t> &exp2);
-void free_program(Program &pg);
+void free_program(Context &ctx, Program &pg);
 
 }  // namespace bnpp

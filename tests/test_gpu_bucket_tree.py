@@ -401,7 +401,7 @@ def test_split_runs_of_two_components_share_launches(ctx, capfd):
             for key in kn:
                 del os.environ[key]
         if "BNPP_DUMP_PLAN" in kn:
-            runs = [ln.split()[0] for ln in capfd.readouterr().err.splitlines() if " n_in=9 " in ln]
+            runs = [ln.split()[0] for ln in capfd.readouterr().err.splitlines() if " chain F=8 " in ln]
             assert runs and max(runs.count(lv) for lv in runs) >= 2, runs
     assert res[1] == res[0] and res[2] == res[0]
     ma, mb = bnpp.Model.from_dict(a), bnpp.Model.from_dict(b)
