@@ -190,7 +190,7 @@ uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<i
     mix((uint64_t)part);
     mix((uint64_t)n_parts);
     // the planner's tuning knobs change the plan and its arena need
-    for (const char *k : {"BNPP_NO_SPLIT", "BNPP_NO_DENSE", "BNPP_SPLIT_MIN_F", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_NO_REDUCE_MANY",
+    for (const char *k : {"BNPP_NO_SPLIT", "BNPP_NO_DENSE", "BNPP_NO_SIMPLE_LEVELS", "BNPP_SIMPLE_MAX", "BNPP_SPLIT_MIN_F", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_NO_REDUCE_MANY",
                           "BNPP_CHAIN_RUN_MAX", "BNPP_NO_CHAIN_FWDV", "BNPP_NO_STREAM", "BNPP_NO_SLAB", "BNPP_MAX_TILE"}) {
         const char *v = std::getenv(k);
         mix(0x9e37u);
@@ -401,8 +401,8 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
         if (timing) {
             int64_t ideal = 0;
             for (const VEPlan *pp : bp) ideal += plan_peak_bytes(*pp, eb);
-            std::fprintf(stderr, "[bnpp] schedule: %zu buckets, ideal live peak %.2f GB, arena %.2f GB\n",
-                         s.descs.size(), ideal / 1e9, s.arena_bytes / 1e9);
+            std::fprintf(stderr, "[bnpp] schedule: %zu buckets, %zu launches, ideal live peak %.2f GB, arena %.2f GB\n",
+                         s.descs.size(), s.groups.size(), ideal / 1e9, s.arena_bytes / 1e9);
         }
         levels += s.n_levels;
         buckets += (double)s.descs.size();

@@ -469,6 +469,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
     // dim (the tile is then v1*v2 contiguous output entries)
     int max_tile = max_vec == 2 ? 8 : 16;
     if (const char *e = std::getenv("BNPP_MAX_TILE")) max_tile = std::max(1, std::min(max_tile, std::atoi(e)));
+    if (b.simple) max_tile = 1;
     auto aligned = [&](int dim, int v) {
         for (int i = 0; i < n; ++i) {
             if (merged[dim].s[i] != 1) continue;
@@ -532,7 +533,8 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         }
         const int eb = max_vec == 2 ? 8 : 4;
         const char *off = std::getenv("BNPP_NO_STREAM");
-        if (!b.divide && n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 && !(off && *off == '1')) {
+        if (!b.simple && !b.divide && n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 &&
+            !(off && *off == '1')) {
             int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
             int64_t s1 = merged.size() < 2 ? 0 : merged[1].s[big];
             // slab form (slab.cuh): the big input is k slabs contiguous along the
@@ -1701,7 +1703,12 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         // equal keys share their top bits: 64 shards sorted and grouped in parallel
         constexpr int kShards = 64;
         std::vector<std::vector<Key>> shard(kShards);
-        for (const Key &k : keys) shard[k.h1 >> 58].push_back(k);
+        {
+            std::vector<size_t> cnt(kShards, 0);
+            for (const Key &k : keys) ++cnt[k.h1 >> 58];
+            for (int sh = 0; sh < kShards; ++sh) shard[sh].reserve(cnt[sh]);
+            for (const Key &k : keys) shard[k.h1 >> 58].push_back(k);
+        }
         parallel_for(kShards, [&](int64_t sh) {
             std::vector<Key> &v = shard[sh];
             std::sort(v.begin(), v.end(), [](const Key &a, const Key &b) {
@@ -1712,6 +1719,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                     canon[v[i].t] = canon[v[i - 1].t];  // the first occurrence (lowest id) of the group
         });
     }
+    const double Td = clk();
     auto remap = [&](size_t pi, int t) { return t < s.n_src ? t : canon[msg_base[pi] + (t - s.n_src)]; };
     // a bucket runs when it produces its table's canonical copy
     auto kept = [&](size_t pi, const BucketSpec &b) {
@@ -1721,20 +1729,29 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     if (dedup) {
         // work actually scheduled: the kept buckets' factor-entries and traffic
         // (plain buckets; a schedule with fused runs keeps the plans' sums)
-        double e = 0, mv = 0;
-        bool plain = true;
-        for (size_t pi = 0; pi < plans.size() && plain; ++pi) {
+        std::vector<double> pe(plans.size(), 0), pm(plans.size(), 0);
+        std::vector<char> pplain(plans.size(), 1);
+        parallel_for((int64_t)plans.size(), [&](int64_t pi) {
             const std::vector<int> &pc = plans[pi]->cards_ext.empty() ? cards : plans[pi]->cards_ext;
             for (const BucketSpec &b : plans[pi]->buckets) {
                 if (!b.chain_x.empty()) {
-                    plain = false;
+                    pplain[pi] = 0;
                     break;
                 }
                 if (!kept(pi, b)) continue;
-                e += (double)table_size(chain_scope(b.in), pc);
-                mv += (double)table_size(b.out_vars, pc);
-                for (const View &v : b.in) mv += (double)table_size(v.vars, pc);
+                // factor-entries: prod(card) over the union scope = output x summed card
+                const double out = (double)table_size(b.out_vars, pc);
+                pe[pi] += out * (b.elim_var >= 0 ? pc[b.elim_var] : 1);
+                pm[pi] += out;
+                for (const View &v : b.in) pm[pi] += (double)table_size(v.vars, pc);
             }
+        });
+        bool plain = true;
+        double e = 0, mv = 0;
+        for (size_t pi = 0; pi < plans.size(); ++pi) {
+            plain = plain && pplain[pi];
+            e += pe[pi];
+            mv += pm[pi];
         }
         if (plain) {
             s.entries = e;
@@ -1745,15 +1762,22 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     // lifetimes: produced level, last consuming level
     const int kForever = INT_MAX;
     std::vector<int> born(s.n_tables, 0), last(s.n_tables, -1);
-    for (size_t pi = 0; pi < plans.size(); ++pi) {
+    // per plan in parallel: a canonical table is born once; its last use is
+    // the latest level of any plan's kept consumer (atomic max)
+    parallel_for((int64_t)plans.size(), [&](int64_t pi) {
         for (const BucketSpec &b : plans[pi]->buckets) {
             if (!kept(pi, b)) continue;
             born[remap(pi, b.out_table)] = b.level;
             for (const View &v : b.in) {
-                int t = remap(pi, v.table);
-                last[t] = std::max(last[t], b.level);
+                int *lt = &last[remap(pi, v.table)];
+                int cur = __atomic_load_n(lt, __ATOMIC_RELAXED);
+                while (cur < b.level &&
+                       !__atomic_compare_exchange_n(lt, &cur, b.level, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+                }
             }
         }
+    });
+    for (size_t pi = 0; pi < plans.size(); ++pi) {
         std::vector<int> res = plans[pi]->results;
         std::vector<std::vector<int>> res_vars = plans[pi]->results_vars;
         if (res.empty()) {                      // single-result plan (PR / one MAR target / VE)
@@ -1851,16 +1875,29 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     for (size_t pi = 0; pi < plans.size(); ++pi)
         for (const BucketSpec &b : plans[pi]->buckets)
             if (kept(pi, b)) items.push_back(Item{b.level, pi, &b, BucketDesc{}, {}, 0, true, {}});
+    // small plain buckets of levels holding several buckets (per-target MAR:
+    // ~9 tile / input-count variants per level, 1018 launches at 12x32) share
+    // one generic 1x1 launch per level: launches, not bytes, bound them
+    int64_t simple_max = 4096;                         // output entries (BNPP_SIMPLE_MAX: tuning)
+    if (const char *e = std::getenv("BNPP_SIMPLE_MAX")) simple_max = std::atoll(e);
+    std::vector<int> lvl_n(n_levels + 2, 0);
+    for (const Item &it : items) ++lvl_n[it.level];
+    const char *ns = std::getenv("BNPP_NO_SIMPLE_LEVELS");
+    const bool simplify = !(ns && *ns == '1');
     parallel_for((int64_t)items.size(), [&](int64_t idx) {
         Item &it = items[idx];
         BucketSpec b = *it.b;
+        b.simple = simplify && lvl_n[it.level] > 1 && b.chain_x.empty() && !b.divide &&
+                   plans[it.plan]->msgs[b.out_table - s.n_src].size <= simple_max;
         for (View &v : b.in) v.table = remap(it.plan, v.table);
         b.out_table = remap(it.plan, b.out_table);
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
         it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf)
                  : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2)
-                 : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2) : variant_key(it.d.n_in, it.d.v1, it.d.v2);
+                 : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2)
+                 : b.simple ? variant_key(kMaxIn, 1, 1)         // the widest input class runs any input count
+                            : variant_key(it.d.n_in, it.d.v1, it.d.v2);
     });
     const double T2 = clk();
     for (const Item &it : items)
@@ -1939,8 +1976,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     // one dims-pool vector per bucket: freed on the worker threads
     parallel_for((int64_t)items.size(), [&](int64_t i) { std::vector<int64_t>().swap(items[i].pool); });
     if (timing)
-        std::fprintf(stderr, "[bnpp] build_schedule: lifetimes %.1f ms, arena %.1f ms, descriptors %.1f ms, grouping %.1f ms\n",
-                     Tl - T0, T1 - Tl, T2 - T1, clk() - T2);
+        std::fprintf(stderr, "[bnpp] build_schedule: dedup %.1f ms, lifetimes %.1f ms, arena %.1f ms, descriptors %.1f ms, "
+                     "grouping %.1f ms\n", Td - T0, Tl - Td, T1 - Tl, T2 - T1, clk() - T2);
     return true;
 }
 

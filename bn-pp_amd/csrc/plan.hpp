@@ -63,6 +63,10 @@ struct BucketSpec {
     std::vector<int> chain_x, chain_n;
     int chain_gmask = 0;
     bool divide = false;            // Factor::divide: in[0] / in[1] (generic kernel, no sum)
+    // build_schedule: a small bucket of a level with several kernel variants
+    // runs in the level's one generic 1x1 launch (launch count, not bandwidth,
+    // bounds such levels)
+    bool simple = false;
 };
 
 // Compile one bucket into a descriptor + dims-pool rows.  max_vec: 4 (fp32) / 2 (fp64).
