@@ -178,6 +178,9 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
     c.neg_e = (int)(-e_sum);
 }
 
+#ifndef BNPP_DENSE_JR
+#define BNPP_DENSE_JR 1       // dense runs: G offsets per tile for the boundary bucket only
+#endif
 #ifndef BNPP_SPLIT_FLAT
 #define BNPP_SPLIT_FLAT 0     // 1: one tile per workgroup (flat grid), no prefetch
 #endif
@@ -195,7 +198,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Persistent workgroups walk the level's tiles (64 rest entries each) grid-
 // stride; the next tile's message loads are issued before the current tile is
 // computed, so HBM stays busy through the exchange barriers and the stores.
-template <int F, int FORM, int DEP, bool DENSE>
+// MULTI: the launch holds several runs (descriptors); otherwise exactly one,
+// and the kernel is the one-run loop only -- without the multi-run path's
+// per-bucket restaging live in the same body, the uniform state fits the
+// scalar registers (with it: ~80 SGPRs spilled to VGPR lanes, re-read per tile)
+template <int F, int FORM, int DEP, bool DENSE, bool MULTI>
 __global__ __launch_bounds__(64 * (1 << (F - 4))) __attribute__((amdgpu_waves_per_eu(BNPP_SPLIT_WAVES > 0 ? BNPP_SPLIT_WAVES : 1)))
 void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const int64_t *__restrict__ pool,
                         TableMeta *__restrict__ meta, int64_t total_vblocks) {
@@ -267,8 +274,11 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 in_off = tin + (int64_t)lane * N;
                 out_off = tout + lane;
             }
+            // only the run's boundary bucket (the last forward, the first
+            // backward) may have a G table varying along rest dim 1 (planner)
+            constexpr int JR = FORM == kChainFwd ? F - 1 : 0;
 #pragma unroll
-            for (int j = 0; j < F; ++j) gb[j] = (int32_t)d1 * c.d_g1[j];
+            for (int j = 0; j < F; ++j) gb[j] = (j == JR || BNPP_DENSE_JR == 0) ? (int32_t)d1 * c.d_g1[j] : 0;
             return;
         }
         const int64_t tid0 = (vb - cur_begin) * kSplitRows;
@@ -492,7 +502,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     float rg[16];
     int64_t in_off, out_off;
     int32_t gb[F];
-    if (n_desc == 1 && BNPP_SPLIT_FLAT == 0 && FORM == kChainBwd) {
+    if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0 && FORM == kChainBwd) {
         // one bucket, backward form: the next tile's loads are issued
         // (unconditionally: the last tile is re-read rather than branching, so
         // the wait counts stay static) before the current tile is computed (a
@@ -511,7 +521,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             vb = vbn;
             if (vb >= total_vblocks) break;
         }
-    } else if (n_desc == 1 && BNPP_SPLIT_FLAT == 0) {
+    } else if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0) {
         // one bucket, forward form: the loads of the next two tiles are in flight while a
         // tile is computed (register sets A and B alternate: a set is copied
         // out only once its loads are two tiles old, so no wait exposes
@@ -582,8 +592,11 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     {
         std::lock_guard<std::mutex> g(ds.mu);
         if (!ds.done[dev]) {
-            ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP, DENSE>,
+            ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP, DENSE, false>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (ds.attr[dev] == hipSuccess)
+                ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP, DENSE, true>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (hipDeviceGetAttribute(&ds.cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
                 ds.cus[dev] <= 0)
                 ds.cus[dev] = 256;
@@ -594,8 +607,12 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     }
     const int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
     const int64_t grid = BNPP_SPLIT_FLAT ? a.vblocks : a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
-    hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP, DENSE>), dim3((unsigned)grid), dim3(64 * split_waves(F)), shm,
-                       stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
+    if (a.n_desc == 1)
+        hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP, DENSE, false>), dim3((unsigned)grid),
+                           dim3(64 * split_waves(F)), shm, stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
+    else
+        hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP, DENSE, true>), dim3((unsigned)grid),
+                           dim3(64 * split_waves(F)), shm, stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
     return hipGetLastError();
 }
 

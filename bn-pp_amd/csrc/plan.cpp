@@ -303,6 +303,9 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         bool dense = !(nd && *nd == '1') && !md.empty() && md.size() <= 2 && md[0].card >= (uint64_t)kSplitRowsHost &&
                      (md[0].card & (md[0].card - 1)) == 0 && (fw ? md[0].in == 1 : md[0].in == N);
         for (int j = 0; dense && j < F; ++j) dense = md[0].g[j] == 0;
+        // along rest dim 1 only the boundary bucket's G may vary (chainsplit.cuh JR)
+        for (int j = 0; dense && md.size() == 2 && j < F; ++j)
+            dense = j == (fw ? F - 1 : 0) || md[1].g[j] == 0;
         const int64_t S = fw ? is[F - 1] : os[0];
         for (int p = 0; dense && p < F; ++p) dense = S > 0 && (fw ? is[p] : os[p]) == (S << (fw ? F - 1 - p : p));
         const int dform = fw ? kChainFwdSD : kChainBwdSD;

@@ -233,11 +233,25 @@ __global__ void fill(float *p, long n) {
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = 0.5f + 0.25f * ((i * 2654435761u) % 1024) / 1024.f;
 }
 
-int main() {
+int main(int argc, char **argv) {
     const int reps = 5;
     float *a, *b, *g;
-    CK(hipMalloc(&a, kTotal * 4)); CK(hipMalloc(&b, kTotal * 4)); CK(hipMalloc(&g, 64 * 4));
+    // argv[1] = GB: both messages inside one allocation of that size, at its
+    // two ends (the engine's 257-GB arena), instead of two 17-GB allocations
+    const double arena_gb = argc > 1 ? atof(argv[1]) : 0;
+    if (arena_gb > 0) {
+        char *big = nullptr;
+        const size_t bytes = (size_t)(arena_gb * 1e9);
+        CK(hipMalloc((void **)&big, bytes));
+        a = (float *)big;
+        b = (float *)(big + ((bytes - kTotal * 4) & ~(size_t)((1 << 21) - 1)));
+        printf("{\"arena_GB\": %.1f}\n", arena_gb);
+    } else {
+        CK(hipMalloc(&a, kTotal * 4)); CK(hipMalloc(&b, kTotal * 4));
+    }
+    CK(hipMalloc(&g, 64 * 4));
     fill<<<4096, 256>>>(a, kTotal);
+    fill<<<4096, 256>>>(b, kTotal);
     fill<<<1, 256>>>(g, 64);
     CK(hipDeviceSynchronize());
     int cus = 0;
@@ -259,16 +273,20 @@ int main() {
         CK(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         run(name, [&] { hipLaunchKernelGGL(k, dim3(cus), dim3(1024), shm, 0, a, b, tiles, g); });
     };
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int rep = 0; rep < (arena_gb > 0 ? 1 : 2); ++rep) {
         run("copy", [&] { copyf<<<kTotal / 1024, 256>>>((const v4f *)a, (v4f *)b); });
         go("fwd_XI_d2", fwd<false, 2>, true);
         go("fwd_XI_d1", fwd<false, 1>, true);
-        go("fwd_RI_d2", fwd<true, 2>, false);
-        go("fwd_RI_d1", fwd<true, 1>, false);
+        if (arena_gb == 0) {
+            go("fwd_RI_d2", fwd<true, 2>, false);
+            go("fwd_RI_d1", fwd<true, 1>, false);
+        }
         go("bwd_XI_d1", bwd<false, 1>, true);
         go("bwd_XI_d2", bwd<false, 2>, true);
-        go("bwd_RI_d1", bwd<true, 1>, false);
-        go("bwd_RI_d2", bwd<true, 2>, false);
+        if (arena_gb == 0) {
+            go("bwd_RI_d1", bwd<true, 1>, false);
+            go("bwd_RI_d2", bwd<true, 2>, false);
+        }
     }
     return 0;
 }
