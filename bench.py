@@ -39,6 +39,7 @@ per-target and bucket-tree MAR, with the largest difference between them.
 (bit-exact path; 17.2 GB per launch), with its own roofline fraction.
 """
 import argparse
+import glob
 import json
 import os
 import subprocess
@@ -354,11 +355,12 @@ def main():
     torch.cuda.empty_cache()
 
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "traffic_r02.json")   # tools/profile_bench.sh, this kernel
-    if os.path.exists(tpath):
+    # newest profiles/traffic_rNN.json (tools/profile_bench.sh) for this kernel
+    for tpath in sorted(glob.glob(os.path.join(REPO, "profiles", "traffic_r*.json")), reverse=True):
         tj = json.load(open(tpath))
         if tj.get("k") == k and tj.get("w") == w and tj.get("dtype") == args.dtype:
             traffic = tj.get("hbm_bytes_per_launch")
+            break
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
