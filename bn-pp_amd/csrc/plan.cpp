@@ -4,10 +4,13 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <map>
 #include <memory_resource>
 #include <set>
 #include <thread>
+#include <unistd.h>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -16,7 +19,75 @@
 
 namespace bnpp {
 
+// Persistent host workers (spawning 15 threads per call cost ~1 ms of a
+// millisecond-scale PR plan).  One parallel_for at a time uses the pool; a
+// concurrent or nested call (another context's thread, a body that itself
+// calls parallel_for) runs on threads of its own as before.
+namespace {
+struct HostPool {
+    std::mutex run_mu;                         // held by the one call using the pool
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::vector<std::thread> workers;
+    const std::function<void(int64_t)> *body = nullptr;
+    std::atomic<int64_t> next{0};
+    int64_t n = 0;
+    uint64_t gen = 0;
+    int want = 0, active = 0;
+    bool stop = false;
+    static thread_local bool in_worker;
+    explicit HostPool(int nw) {
+        for (int i = 0; i < nw; ++i) workers.emplace_back([this, i] { loop(i); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto &t : workers) t.join();
+    }
+    void drain() {
+        for (int64_t i = next++; i < n; i = next++) (*body)(i);
+    }
+    void loop(int id) {
+        in_worker = true;
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || (gen != seen && id < want); });
+            if (stop) return;
+            seen = gen;
+            lk.unlock();
+            drain();
+            lk.lock();
+            if (--active == 0) done_cv.notify_all();
+        }
+    }
+    void run(int64_t count, const std::function<void(int64_t)> &fn, int helpers) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            body = &fn;
+            n = count;
+            next = 0;
+            want = helpers;
+            active = helpers;
+            ++gen;
+        }
+        cv.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu);
+        done_cv.wait(lk, [&] { return active == 0; });
+        body = nullptr;
+    }
+};
+thread_local bool HostPool::in_worker = false;
+}  // namespace
+
+thread_local int t_host_threads = 0;            // ScopedHostThreads
+
 void parallel_for(int64_t n, const std::function<void(int64_t)> &body, int threads) {
+    if (threads <= 0) threads = t_host_threads;
     if (threads <= 0) {
         threads = (int)std::thread::hardware_concurrency();
         if (const char *e = std::getenv("BNPP_HOST_THREADS")) threads = std::atoi(e);
@@ -26,15 +97,26 @@ void parallel_for(int64_t n, const std::function<void(int64_t)> &body, int threa
         for (int64_t i = 0; i < n; ++i) body(i);
         return;
     }
+    const int nt = (int)std::min<int64_t>(threads, n);
+    // never destroyed (workers may outlive static teardown); a forked child
+    // has the object but not its threads, so it uses threads of its own
+    static HostPool *pool = new HostPool(15);
+    static const pid_t pool_pid = getpid();
+    if (!HostPool::in_worker && nt - 1 <= (int)pool->workers.size() && getpid() == pool_pid) {
+        std::unique_lock<std::mutex> g(pool->run_mu, std::try_to_lock);
+        if (g.owns_lock()) {
+            pool->run(n, body, nt - 1);
+            return;
+        }
+    }
     std::atomic<int64_t> next(0);
     auto worker = [&]() {
         for (int64_t i = next++; i < n; i = next++) body(i);
     };
-    std::vector<std::thread> pool;
-    int nt = (int)std::min<int64_t>(threads, n);
-    for (int t = 1; t < nt; ++t) pool.emplace_back(worker);
+    std::vector<std::thread> extra;
+    for (int t = 1; t < nt; ++t) extra.emplace_back(worker);
     worker();
-    for (auto &t : pool) t.join();
+    for (auto &t : extra) t.join();
 }
 
 std::vector<int64_t> natural_strides(const std::vector<int> &vars, const std::vector<int> &cards) {
@@ -1626,6 +1708,11 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     const bool timing = std::getenv("BNPP_TIMING") != nullptr;
     auto clk = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double T0 = clk();
+    // small schedules (a PR over a few thousand buckets) build faster on one
+    // thread than the workers' hand-off costs
+    int64_t n_buckets_all = 0;
+    for (const VEPlan *p : plans) n_buckets_all += (int64_t)p->buckets.size();
+    ScopedHostThreads one_thread(n_buckets_all < 8192 ? 1 : 0);
     s.n_src = (int)src_sizes.size();
     s.table_size = src_sizes;
     s.table_offset.assign(src_sizes.size(), -1);

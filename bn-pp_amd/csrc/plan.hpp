@@ -15,6 +15,13 @@ namespace bnpp {
 // Run body(i) for i in [0, n) on up to `threads` host threads (0: hardware
 // concurrency, capped at 16 — the per-GPU CPU share of the target machines).
 void parallel_for(int64_t n, const std::function<void(int64_t)> &body, int threads = 0);
+// parallel_for calls on this thread with threads = 0 use `n` threads while in scope (0: default)
+extern thread_local int t_host_threads;
+struct ScopedHostThreads {
+    int saved;
+    explicit ScopedHostThreads(int n) : saved(t_host_threads) { t_host_threads = n; }
+    ~ScopedHostThreads() { t_host_threads = saved; }
+};
 
 // A table as one bucket input sees it: table id, evidence base offset, and the
 // (variable, stride) pairs that remain after conditioning (domain.cpp:74-90).

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """The reference's larger networks (Pigs, Link, Munin1-4, Barley, Mildew,
 Diabetes; tests/golden/corpus_golden.json): PR (min-fill, fp64) on the device
-against BN::partition timed on this box's CPU (oracle/_ref/ref_harness, one
-core; cases the golden run found slower than --ref-cap seconds keep the build
-container's time), plus all marginals from one bucket tree (fp64), for which
+against BN::partition timed on this box's CPU (oracle/_ref/ref_harness pinned
+to one core with taskset -c 0, median of --ref-reps runs; cases the golden run
+found slower than --ref-cap seconds keep the build container's time), plus all marginals from one bucket tree (fp64), for which
 the reference would run one VE per variable (model.cpp:326-334: ~n_vars x PR).
 
     python tools/corpus_bench.py > gpurun_out/corpus_bench.jsonl
@@ -11,6 +11,8 @@ the reference would run one VE per variable (model.cpp:326-334: ~n_vars x PR).
 import argparse
 import json
 import os
+import platform
+import shutil
 import statistics
 import subprocess
 import sys
@@ -23,11 +25,27 @@ MODELS = os.path.join(REPO, "tests", "golden", "models")
 HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
 
 
-def ref_pr_ms(model, ev):
-    out = subprocess.run([HARNESS, "pr", os.path.join(MODELS, model), os.path.join(MODELS, ev) if ev != "-" else "-",
-                          "mf"], capture_output=True, text=True, timeout=300, check=True).stdout
-    kv = dict(line.split()[:2] for line in out.splitlines() if len(line.split()) == 2)
-    return float(kv["uptime_ms"])
+def ref_pr_ms(model, ev, reps):
+    cmd = [HARNESS, "pr", os.path.join(MODELS, model), os.path.join(MODELS, ev) if ev != "-" else "-", "mf"]
+    if shutil.which("taskset"):
+        cmd = ["taskset", "-c", "0"] + cmd
+    ts = []
+    for _ in range(reps):
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True).stdout
+        kv = dict(line.split()[:2] for line in out.splitlines() if len(line.split()) == 2)
+        ts.append(float(kv["uptime_ms"]))
+    return statistics.median(ts), ts
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
 
 
 def timed(fn, reps=3):
@@ -42,7 +60,11 @@ def timed(fn, reps=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref-cap", type=float, default=60.0, help="seconds: slower reference runs are not re-timed")
+    ap.add_argument("--ref-reps", type=int, default=3)
     args = ap.parse_args()
+    print(json.dumps({"host": {"cpu_model": cpu_model(), "nproc": os.cpu_count(),
+                               "ref_pinning": "taskset -c 0" if shutil.which("taskset") else "none",
+                               "ref_reps": args.ref_reps, "gpu_reps": 3, "statistic": "median"}}), flush=True)
     with open(os.path.join(REPO, "tests", "golden", "corpus_golden.json")) as f:
         cases = json.load(f)["cases"]
     ctx = bnpp.Context(0)
@@ -54,7 +76,8 @@ def main():
                "ref_log10Z": c["log10Z"], "abs_err_log10Z": abs(lz - c["log10Z"]), "gpu_uptime_ms": pr_ms,
                "ref_width": c["ref_width"]}
         if c["ref_uptime_ms"] <= args.ref_cap * 1e3 and os.path.exists(HARNESS):
-            rec["ref_ms"], rec["ref_where"] = ref_pr_ms(c["model"], c["evidence"]), "this box"
+            rec["ref_ms"], rec["ref_samples_ms"] = ref_pr_ms(c["model"], c["evidence"], args.ref_reps)
+            rec["ref_where"] = "this box"
         else:
             rec["ref_ms"], rec["ref_where"] = c["ref_uptime_ms"], "build container (golden run)"
         rec["speedup"] = rec["ref_ms"] / pr_ms
