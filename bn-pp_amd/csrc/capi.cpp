@@ -43,7 +43,8 @@ struct bnpp_job {
     std::vector<int> targets;
     std::vector<int> ev_val;          // per variable, -1 = no evidence
     std::vector<int> cards;
-    double stats[8] = {0};
+    int n_slices = 1, slice_rank = 0;  // message-sliced bucket tree (bnpp_marginals_tree_sliced)
+    double stats[10] = {0};            // bnpp_job_stats [0..8), then n_xchg, exchange bytes sent
 };
 
 namespace {
@@ -173,7 +174,7 @@ SlotMemo &slot_memo() {
     return m;
 }
 uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<int>> &scopes, const std::vector<int> &ord,
-                  const std::vector<int> &targets, int eb, int chain_eb, int part, int n_parts) {
+                  const std::vector<int> &targets, int eb, int chain_eb, int part, int n_parts, int n_slices) {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
     auto mixv = [&](const std::vector<int> &v) {
@@ -189,9 +190,10 @@ uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<i
     mix((uint64_t)chain_eb);              // fused runs on/off change the plan
     mix((uint64_t)part);
     mix((uint64_t)n_parts);
+    mix((uint64_t)n_slices);              // the slice rank does not change the arena need
     // the planner's tuning knobs change the plan and its arena need
     for (const char *k : {"BNPP_NO_SPLIT", "BNPP_NO_DENSE", "BNPP_NO_SIMPLE_LEVELS", "BNPP_SIMPLE_MAX", "BNPP_SPLIT_MIN_F", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_NO_REDUCE_MANY",
-                          "BNPP_CHAIN_RUN_MAX", "BNPP_NO_CHAIN_FWDV", "BNPP_NO_STREAM", "BNPP_NO_SLAB", "BNPP_MAX_TILE"}) {
+                          "BNPP_CHAIN_RUN_MAX", "BNPP_NO_CHAIN_FWDV", "BNPP_NO_STREAM", "BNPP_NO_SLAB", "BNPP_MAX_TILE", "BNPP_SLICE_MIN_WIN"}) {
         const char *v = std::getenv(k);
         mix(0x9e37u);
         for (const char *c = v ? v : ""; *c; ++c) mix((unsigned char)*c);
@@ -202,7 +204,7 @@ uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<i
 // Build the VE plans for a job: kind 0 = partition, kind 1 = marginals of targets.
 int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
                 int n_order, const std::vector<int> &targets, std::vector<VEPlan> &plans, int &max_width,
-                int64_t budget, int eb, int part = 0, int n_parts = 1) {
+                int64_t budget, int eb, int part = 0, int n_parts = 1, int n_slices = 1, int slice_rank = 0) {
     const int nv = (int)d.cards.size();
     auto scopes = conditioned_scopes(d, ev);
     auto views = source_views(d, ev);
@@ -261,16 +263,18 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
         if (force && std::atoi(force) > 0) {
             std::string msg;
             VEPlan cp;
-            if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), part, n_parts, cp, &msg, chain_eb))
+            if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), part, n_parts, cp, &msg, chain_eb,
+                                        n_slices, slice_rank))
                 return set_err(BNPP_ERR_UNSUPPORTED, msg);
             plans.back() = std::move(cp);
-        } else if (need(plans.back()) > budget || n_parts > 1) {
+        } else if (need(plans.back()) > budget || n_parts > 1 || n_slices > 1) {
             // every forward message does not fit: recompute them from checkpoints
             // (chain-shaped trees), with as many checkpoint slots as fit
             std::string msg;
             VEPlan best;
-            int lo = 1, hi = 64, best_s = 0;
-            const uint64_t key = slot_key(d.cards, scopes, ord, targets, eb, chain_eb, part, n_parts);
+            // sliced messages are 1/n_slices of the size: room for more checkpoints
+            int lo = 1, hi = n_slices > 1 ? 256 : 64, best_s = 0;
+            const uint64_t key = slot_key(d.cards, scopes, ord, targets, eb, chain_eb, part, n_parts, n_slices);
             int memo_s = 0;
             {
                 std::lock_guard<std::mutex> g(slot_memo().mu);
@@ -279,7 +283,8 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             }
             if (memo_s > 0) {                             // the search would land on the same count
                 VEPlan cp;
-                if (plan_bucket_tree_chain(d.cards, views, ord, targets, memo_s, part, n_parts, cp, &msg, chain_eb) &&
+                if (plan_bucket_tree_chain(d.cards, views, ord, targets, memo_s, part, n_parts, cp, &msg, chain_eb, n_slices,
+                                           slice_rank) &&
                     need(cp) <= budget) {
                     best_s = memo_s;
                     best = std::move(cp);
@@ -291,7 +296,8 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             while (lo <= hi) {
                 int mid = (lo + hi) / 2;
                 VEPlan cp;
-                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, part, n_parts, cp, &msg, chain_eb)) {
+                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, part, n_parts, cp, &msg, chain_eb, n_slices,
+                                            slice_rank)) {
                     exact = false;
                     break;
                 }
@@ -315,6 +321,9 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                 }
                 if (std::getenv("BNPP_TIMING")) std::fprintf(stderr, "[bnpp] bucket tree: %d checkpoint slots\n", best_s);
                 plans.back() = std::move(best);
+            } else if (n_slices > 1) {
+                return set_err(msg.empty() ? BNPP_ERR_OOM : BNPP_ERR_UNSUPPORTED,
+                               msg.empty() ? "sliced bucket tree: no checkpoint count fits the memory budget" : msg);
             }
         }
     } else {
@@ -352,13 +361,15 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
 // arenas fit `budget` bytes; a batch runs as one level-aligned schedule.
 int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
                    int n_order, const std::vector<int> &targets, int dtype, int64_t budget,
-                   std::vector<Schedule> &out, double *stats, int part = 0, int n_parts = 1) {
+                   std::vector<Schedule> &out, double *stats, int part = 0, int n_parts = 1, int n_slices = 1,
+                   int slice_rank = 0) {
     std::vector<VEPlan> plans;
     int width = 0;
     const bool timing = std::getenv("BNPP_TIMING") != nullptr;
     double t0 = now_ms();
     const int eb = dtype == BNPP_F32 ? 4 : 8;
-    int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width, budget, eb, part, n_parts);
+    int rc = build_plans(d, ev, kind, heuristic, order, n_order, targets, plans, width, budget, eb, part, n_parts,
+                         n_slices, slice_rank);
     if (rc) return rc;
     if (timing) std::fprintf(stderr, "[bnpp] plans %.1f ms\n", now_ms() - t0);
     std::vector<int64_t> src_sizes;
@@ -419,6 +430,13 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
     stats[5] = (double)mx;
     stats[6] = moved * eb;
     stats[7] = (double)out.size();
+    double nx = 0, xe = 0;
+    for (auto &p : plans) {
+        nx += p.n_xchg;
+        xe += p.xchg_elems;
+    }
+    stats[8] = nx;
+    stats[9] = xe * eb;
     // the plans hold millions of small vectors (per-target MAR: one plan per
     // target, ~25 ms to free): a background thread frees them while the call
     // goes on to upload and launch (plans of one bucket tree: here)
@@ -450,7 +468,8 @@ int64_t memory_budget(bnpp_ctx *ctx, bool use_cache = false) {
 
 int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals,
                int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
-               std::unique_ptr<bnpp_job> &job, int part = 0, int n_parts = 1, bool use_cache = false) {
+               std::unique_ptr<bnpp_job> &job, int part = 0, int n_parts = 1, bool use_cache = false, int n_slices = 1,
+               int slice_rank = 0, int64_t budget = 0) {
     if (!ctx || !m) return set_err(BNPP_ERR_INVALID, "null context or model");
     if (dtype != BNPP_F32 && dtype != BNPP_F64) return set_err(BNPP_ERR_INVALID, "bad dtype");
     const ModelData &d = m->d;
@@ -458,6 +477,8 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     job->ctx = ctx;
     job->kind = kind;
     job->cards = d.cards;
+    job->n_slices = n_slices;
+    job->slice_rank = slice_rank;
     std::string msg;
     if (!evidence_array(d, n_ev, ev_vars, ev_vals, job->ev_val, msg)) return set_err(BNPP_ERR_INVALID, msg);
     if (kind == 1 || kind == 3) {
@@ -473,8 +494,9 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     std::vector<Schedule> batches;
     if (n_parts < 1 || part < 0 || part >= n_parts) return set_err(BNPP_ERR_INVALID, "bad part / n_parts");
     const double tp = now_ms();
-    int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype, memory_budget(ctx, use_cache),
-                            batches, job->stats, part, n_parts);
+    int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype,
+                            budget > 0 ? budget : memory_budget(ctx, use_cache), batches, job->stats, part, n_parts,
+                            n_slices, slice_rank);
     if (rc) return rc;
     const double t0 = now_ms();
     rc = upload_sources(ctx->c, d.values, dtype == BNPP_F32 ? kF32 : kF64, job->src);
@@ -542,6 +564,52 @@ int job_results(bnpp_job *job, hipStream_t stream, double *out, double *z_out, i
         } else {                                        // variable in no factor
             for (int s = 0; s < k; ++s) out[o + s] = 1.0 / k;
         }
+        o += (size_t)k;
+    }
+    return BNPP_OK;
+}
+
+// results of a launched sliced job: this rank's share of every target's
+// unnormalised marginal, as mantissas (out, sum(card)) and a power-of-two
+// scale per target (out_exp2; kNoExp when the share is zero).  Evidence
+// variables and variables in no factor: rank 0 carries the one-hot / uniform
+// table.  A target that is a slice variable where it is delivered has a
+// scalar share, at the index its value (the rank's bit) selects.
+constexpr int64_t kNoExp = -((int64_t)1 << 40);
+int job_results_sliced(bnpp_job *job, hipStream_t stream, double *out, int64_t *out_exp2) {
+    std::vector<std::vector<double>> vals;
+    std::vector<int64_t> exp2;
+    int rc = fetch_program(job->ctx->c, job->pg, stream, vals, exp2);
+    if (rc) return from_ctx(job->ctx, rc);
+    std::vector<const std::vector<int> *> rvars;
+    std::vector<int> sbit;
+    for (auto &ex : job->pg.parts) {
+        for (auto &v : ex.sched.plan_result_vars) rvars.push_back(&v);
+        for (int b : ex.sched.plan_result_slice_bit) sbit.push_back(b);
+    }
+    const bool lead = job->slice_rank == 0;
+    size_t o = 0;
+    for (size_t i = 0; i < job->targets.size(); ++i) {
+        const int t = job->targets[i], k = job->cards[t];
+        const std::vector<double> &r = vals[i];
+        const int sb = i < sbit.size() ? sbit[i] : -1;
+        int64_t e = exp2[i];
+        for (int s = 0; s < k; ++s) out[o + s] = 0.0;
+        if (job->ev_val[t] >= 0) {                      // evidence variable: one-hot
+            if (lead) out[o + job->ev_val[t]] = 1.0;
+            e = 0;
+        } else if (sb >= 0 && r.size() == 1) {          // slice variable: the rank's value
+            out[o + ((job->slice_rank >> sb) & 1)] = r[0];
+        } else if ((int)r.size() == k && k > 0 && rvars[i]->size() == 1) {
+            for (int s = 0; s < k; ++s) out[o + s] = r[s];
+        } else {                                        // variable in no factor: uniform
+            if (lead)
+                for (int s = 0; s < k; ++s) out[o + s] = 1.0 / k;
+            e = 0;
+        }
+        bool any = false;
+        for (int s = 0; s < k; ++s) any = any || out[o + s] != 0.0;
+        out_exp2[i] = any ? e : kNoExp;
         o += (size_t)k;
     }
     return BNPP_OK;
@@ -947,7 +1015,7 @@ int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars,
     if (kind == 1 || kind == 3)
         for (int v = 0; v < (int)m->d.cards.size(); ++v) targets.push_back(v);
     std::vector<Schedule> batches;
-    double st[8] = {0};
+    double st[10] = {0};
     int rc = plan_schedules(m->d, ev, kind, heuristic, order, n_order, targets, dtype, memory_budget(nullptr), batches, st);
     if (rc) return rc;
     for (int i = 0; i < n_stats && i < 8; ++i) stats[i] = st[i];
@@ -966,7 +1034,7 @@ int bnpp_plan_tree_part(const bnpp_model *m, int n_ev, const int *ev_vars, const
     if (!evidence_array(m->d, n_ev, ev_vars, ev_vals, ev, msg)) return set_err(BNPP_ERR_INVALID, msg);
     for (int v = 0; v < (int)m->d.cards.size(); ++v) targets.push_back(v);
     std::vector<Schedule> batches;
-    double st[8] = {0};
+    double st[10] = {0};
     int rc = plan_schedules(m->d, ev, 3, heuristic, order, n_order, targets, dtype, memory_budget(nullptr), batches, st,
                             part, n_parts);
     if (rc) return rc;
@@ -1088,6 +1156,84 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
                      t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
     if (rc) return rc;
     if (uptime_ms) *uptime_ms = now_ms() - t0;
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+int bnpp_marginals_tree_sliced(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                               int heuristic, const int *order, int n_order, int n_targets, const int *targets,
+                               int rank, int n_ranks, bnpp_collective_fn coll, void *user, double budget_gb,
+                               int dtype, double *out, int64_t *out_exp2, double *uptime_ms) {
+    BNPP_GUARD_BEGIN
+    if (!out || !out_exp2 || !coll) return set_err(BNPP_ERR_INVALID, "null output or collective");
+    if (n_ranks < 2) return set_err(BNPP_ERR_INVALID, "sliced runs need n_ranks >= 2 (bnpp_marginals_tree otherwise)");
+    double t0 = now_ms();
+    std::unique_ptr<bnpp_job> job;
+    std::unique_lock<std::mutex> lk;
+    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
+    int rc = create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job,
+                        0, 1, lk.owns_lock(), n_ranks, rank, budget_gb > 0 ? (int64_t)(budget_gb * 1e9) : 0);
+    const double t1 = now_ms();
+    if (rc == BNPP_OK) {
+        job->pg.hooks.fn = coll;
+        job->pg.hooks.user = user;
+        rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
+    }
+    const double t2 = now_ms();
+    if (rc == BNPP_OK) rc = job_results_sliced(job.get(), ctx->c.stream, out, out_exp2);
+    const double t3 = now_ms();
+    if (job) destroy_job(job.release());
+    record_call_timing(t0, t1, t2, t3);
+    if (std::getenv("BNPP_TIMING"))
+        std::fprintf(stderr, "[bnpp] sliced tree marginals (rank %d of %d): create %.1f ms, launch %.1f ms, run+fetch %.1f ms\n",
+                     rank, n_ranks, t1 - t0, t2 - t1, t3 - t2);
+    if (rc) return rc;
+    if (uptime_ms) *uptime_ms = now_ms() - t0;
+    return BNPP_OK;
+    BNPP_GUARD_END
+}
+
+// a world of n_ranks identical ranks (user: int[2] = {n_ranks, flags}):
+// every block this rank would receive is a copy of what it sends -- the
+// timing of one rank's share of a sliced run on one GPU, the data movement
+// local; flags & 1: no bytes move (the exchanges' transfer time left out)
+int bnpp_collective_loopback(void *user, int op, const void *send, void *recv, int64_t bytes, void *stream) {
+    if (!user || !send || !recv || bytes < 0) return 1;
+    const int R = static_cast<const int *>(user)[0];
+    if (static_cast<const int *>(user)[1] & 1) return 0;    // no data movement: the compute alone
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (op == BNPP_COLL_ALLGATHER) {
+        for (int r = 0; r < R; ++r)
+            if (hipMemcpyAsync(static_cast<char *>(recv) + (int64_t)r * bytes, send, (size_t)bytes,
+                               hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return 1;
+        return 0;
+    }
+    if (op == BNPP_COLL_ALLTOALL)
+        return hipMemcpyAsync(recv, send, (size_t)bytes * R, hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : 1;
+    return 1;
+}
+
+int bnpp_plan_tree_sliced(const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
+                          const int *order, int n_order, int rank, int n_ranks, int dtype, int *slice_bit,
+                          double *stats, int n_stats) {
+    BNPP_GUARD_BEGIN
+    if (!m) return set_err(BNPP_ERR_INVALID, "null argument");
+    if (n_ranks < 2 || rank < 0 || rank >= n_ranks) return set_err(BNPP_ERR_INVALID, "bad rank / n_ranks");
+    std::vector<int> ev, targets;
+    std::string msg;
+    if (!evidence_array(m->d, n_ev, ev_vars, ev_vals, ev, msg)) return set_err(BNPP_ERR_INVALID, msg);
+    for (int v = 0; v < (int)m->d.cards.size(); ++v) targets.push_back(v);
+    std::vector<Schedule> batches;
+    double st[10] = {0};
+    int rc = plan_schedules(m->d, ev, 3, heuristic, order, n_order, targets, dtype, memory_budget(nullptr), batches, st,
+                            0, 1, n_ranks, rank);
+    if (rc) return rc;
+    size_t i = 0;
+    for (auto &s : batches)
+        for (int b : s.plan_result_slice_bit)
+            if (slice_bit) slice_bit[i++] = b;
+    for (int k = 0; stats && k < n_stats && k < 10; ++k) stats[k] = st[k];
     return BNPP_OK;
     BNPP_GUARD_END
 }

@@ -854,6 +854,26 @@ struct PlanBuilder {
         p.buckets.push_back(b);
         return b.out_table;
     }
+    // one step of a message exchange (BucketSpec::xchg): no arithmetic, its
+    // traffic counted (the sync step's few bytes are not)
+    int push_xchg(const std::vector<View> &in, const std::vector<int> &ov, int kind, int mode, int blocks) {
+        BucketSpec b;
+        b.in = in;
+        b.elim_var = -1;
+        b.out_vars = ov;
+        b.out_table = new_msg(ov);
+        b.xchg = kind;
+        b.xchg_mode = mode;
+        b.xchg_blocks = blocks;
+        int lv = sequential ? last_level : 0;
+        for (const View &v : in) lv = std::max(lv, level[v.table]);
+        b.level = lv + 1;
+        last_level = std::max(last_level, b.level);
+        level[b.out_table] = b.level;
+        if (kind != kXchgSync) p.elems_moved += moved_of({in[0]}, b.out_table);
+        p.buckets.push_back(b);
+        return b.out_table;
+    }
     // a bucket over `in` (any length) summing out `x` (-1: none); inputs past
     // kMaxIn are folded into materialised products left to right, like the
     // reference's chain
@@ -1263,12 +1283,22 @@ int64_t binom_capped(int n, int k) {             // C(n, k), saturating at 2^40
 
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
-                            int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb) {
+                            int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb, int n_slices,
+                            int slice_rank) {
     if (n_parts < 1 || part < 0 || part >= n_parts) {
         if (msg) *msg = "bad part";
         return false;
     }
+    int sbits = 0;
+    while ((1 << sbits) < n_slices && sbits < 16) ++sbits;
+    if (n_slices < 1 || (1 << sbits) != n_slices || slice_rank < 0 || slice_rank >= n_slices ||
+        (n_slices > 1 && n_parts != 1)) {
+        if (msg) *msg = "bad slicing: n_slices must be a power of two, 0 <= rank < n_slices, one part";
+        return false;
+    }
     VEPlan p;
+    p.n_slices = n_slices;
+    p.slice_rank = slice_rank;
     PlanBuilder B(cards, p, sources, order, true);
     B.sequential = true;
     B.chain_eb = chain_eb;
@@ -1298,13 +1328,9 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             child[par] = i;
         }
     }
-    std::vector<int> result_of(cards.size(), -1);
-    // the forward message of bucket i from its child's message (or none)
-    auto forward = [&](int i, const View *lam_child) {
-        std::vector<View> in = src_in[i];
-        if (lam_child) in.push_back(*lam_child);
-        return B.view(B.emit(in, order[i], false));
-    };
+    std::vector<int> result_of(cards.size(), -1), slice_bit_of(cards.size(), -1);
+    bool ok = true;
+    std::string fail_msg;
     auto reduce_to = [&](std::vector<View> in, int t) { return B.reduce_to(std::move(in), t); };
     // paths (leaf ... root); marginals are owned by contiguous segments of the
     // concatenated paths, one segment per part
@@ -1355,6 +1381,133 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         off += m;
         if (a >= b) continue;
         for (int q = a; q < b; ++q) owned_var[order[path[q]]] = 1;
+        // ---- message slicing (n_slices > 1) ----
+        // windows: win[j] = the window of position j (-1: every rank holds the
+        // whole message), Sw[k] its slice variables (canonical order; S[i]'s
+        // value on rank r is bit sbits-1-i of r, so the rank is the block index
+        // of the slice variables read as a mixed-radix number, slowest first).
+        // A window opens at a boundary position e with the b latest-eliminated
+        // variables of sep_e (binary), and lasts while they stay in the
+        // separators: on a grid's column sweep ~30 positions.
+        std::vector<int> win(m, -1);
+        std::vector<std::vector<int>> Sw;
+        if (sbits > 0) {
+            const char *mw = std::getenv("BNPP_SLICE_MIN_WIN");
+            const int min_win = mw ? std::max(1, std::atoi(mw)) : 8;
+            auto top_b = [&](int j, std::vector<int> &S) {
+                const std::vector<int> &sep = lam_vars[path[j]];
+                if ((int)sep.size() < 2 * sbits) return false;
+                S.assign(sep.end() - sbits, sep.end());
+                for (int v : S)
+                    if (cards[v] != 2 || B.rank[v] < 0) return false;
+                return true;
+            };
+            auto in_sep = [&](int j, const std::vector<int> &S) {
+                for (int v : S)
+                    if (!contains(lam_vars[path[j]], v)) return false;
+                return true;
+            };
+            int j = 0;
+            while (j + 1 < m) {
+                std::vector<int> S;
+                bool can = top_b(j, S);
+                if (can && win[j] >= 0)                          // re-slice: the new set avoids the old
+                    for (int v : S) can = can && !contains(Sw[win[j]], v);
+                int f = j;
+                while (can && f + 1 < m && in_sep(f + 1, S)) ++f;
+                if (!can || f - j < min_win) {
+                    ++j;
+                    continue;
+                }
+                for (int q = j + 1; q <= f; ++q) win[q] = (int)Sw.size();
+                Sw.push_back(S);
+                j = f;
+            }
+        }
+        static const std::vector<int> kNoSlice;
+        auto Sof = [&](int w) -> const std::vector<int> & { return w < 0 ? kNoSlice : Sw[w]; };
+        // a view with the slice variables S fixed to this rank's bits
+        auto cond = [&](const View &v, const std::vector<int> &S) {
+            if (S.empty()) return v;
+            View w;
+            w.table = v.table;
+            w.base = v.base;
+            for (size_t i = 0; i < v.vars.size(); ++i) {
+                auto it = std::find(S.begin(), S.end(), v.vars[i]);
+                if (it == S.end()) {
+                    w.vars.push_back(v.vars[i]);
+                    w.strides.push_back(v.strides[i]);
+                } else {
+                    const int bit = sbits - 1 - (int)(it - S.begin());
+                    w.base += (int64_t)((slice_rank >> bit) & 1) * v.strides[i];
+                }
+            }
+            return w;
+        };
+        // the factor tables of the bucket at position q, as its window's ranks see them
+        auto src_at = [&](int q) {
+            std::vector<View> r;
+            for (const View &v : src_in[path[q]]) r.push_back(cond(v, Sof(win[q])));
+            return r;
+        };
+        // the message at position pos (sliced for window wf) re-sliced for window wt
+        auto xchg = [&](View cur, int pos, int wf, int wt) -> View {
+            if (wf == wt || !ok) return cur;
+            const std::vector<int> &So = Sof(wf), &Sn = Sof(wt);
+            if (So.empty()) return cond(cur, Sn);             // whole -> slice: a conditioned view
+            if (cur.table < p.n_src || cur.base != 0 || cur.vars != p.msgs[cur.table - p.n_src].vars)
+                cur = B.view(B.emit({cur}, -1, false));        // exchange whole message tables only
+            const std::vector<int> &A = cur.vars;
+            std::vector<int> rest, sendv;
+            int pmode = 0;
+            if (!Sn.empty()) {
+                for (int v : A)
+                    if (!contains(Sn, v)) rest.push_back(v);
+                const bool slow = A.size() >= Sn.size() && std::equal(Sn.begin(), Sn.end(), A.begin());
+                const bool fast = A.size() >= Sn.size() && std::equal(Sn.begin(), Sn.end(), A.end() - Sn.size());
+                if (!slow && !fast) {
+                    ok = false;
+                    fail_msg = "slicing: the new slice variables are not the slowest or fastest of the message";
+                    return cur;
+                }
+                pmode = slow ? 0 : 1;
+                sendv = Sn;
+                sendv.insert(sendv.end(), rest.begin(), rest.end());
+            } else {
+                sendv = A;
+            }
+            const int vx = (int)B.cards.size();                // scratch: n_slices + 1 int64 exponents
+            B.cards.push_back(2 * (n_slices + 1));
+            B.rank.push_back(-1);
+            const int X = B.push_xchg({cur}, {vx}, kXchgSync, 0, n_slices);
+            const int Ts = B.push_xchg({cur, B.view(X)}, sendv, kXchgPack, pmode, n_slices);
+            const std::vector<int> &within = Sn.empty() ? A : rest;
+            std::vector<int> recvv = So;
+            recvv.insert(recvv.end(), within.begin(), within.end());
+            const int Tr = B.push_xchg({B.view(Ts)}, recvv, kXchgComm, Sn.empty() ? 1 : 0, n_slices);
+            ++p.n_xchg;
+            const double ssz = (double)table_size(sendv, B.cards);
+            p.xchg_elems += Sn.empty() ? ssz * (n_slices - 1) : ssz * (n_slices - 1) / n_slices;
+            std::vector<int> want;
+            for (int v : lam_vars[path[pos]])
+                if (!contains(Sn, v)) want.push_back(v);
+            want = B.canon(want);
+            if (want == recvv) return B.view(Tr);
+            std::vector<int> tl = within;                      // source blocks fastest: a transpose
+            tl.insert(tl.end(), So.begin(), So.end());
+            if (want != tl) {
+                ok = false;
+                fail_msg = "slicing: the old slice variables are not the slowest or fastest of the message";
+                return cur;
+            }
+            return B.view(B.push_xchg({B.view(Tr)}, want, kXchgUnpack, 1, n_slices));
+        };
+        // the forward message of the bucket at position q from the previous one's (or none)
+        auto forward = [&](int q, const View *lam_child) {
+            std::vector<View> in = src_at(q);
+            if (lam_child) in.push_back(*lam_child);
+            return B.view(B.emit(in, order[path[q]], false));
+        };
         // kept sets K_j and the slow parts, per position
         std::vector<std::vector<int>> slow(std::max(m - 1, 0));
         for (int j = 0; j + 1 < m; ++j) slow[j] = slow_part(lam_vars[path[j]]);
@@ -1403,8 +1556,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         int pi_pos = m - 1;
         auto pi_step = [&](int j) {                  // pi_j = sum F_{j+1} * pi_{j+1} down to sep_j
             const std::vector<int> &sep_j = lam_vars[path[j]];
-            const int q = path[j + 1];
-            std::vector<View> in = src_in[q];
+            std::vector<View> in = src_at(j + 1);
             if (have_pi) in.push_back(pi_cur);
             if (in.empty()) {
                 have_pi = false;
@@ -1426,15 +1578,18 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         auto pi_down_to = [&](int j) {
             int jj = pi_pos - 1;
             while (jj >= j) {
+                // buckets jj+1, jj, ... of one slicing window (a run may not cross an exchange)
+                int span = 1;
+                while (jj - span >= j && win[jj + 1 - span] == win[jj + 1]) ++span;
                 // longest fusable run of backward buckets jj, jj-1, ... (chain.cuh)
                 int fused = 0;
-                for (int F = chain_first_try(jj - j + 1); F >= 2 && have_pi && !fused; --F) {
-                    if ((jj - j + 1) - F == 1 && F > 2) continue;   // never strand one bucket
+                for (int F = chain_first_try(span); F >= 2 && have_pi && !fused; --F) {
+                    if (span - F == 1 && F > 2) continue;   // never strand one bucket
                     std::vector<PlanBuilder::ChainStep> steps;
                     std::vector<int> vars = pi_cur.vars;
                     for (int i = 0; i < F; ++i) {
                         const std::vector<int> &sep = lam_vars[path[jj - i]];
-                        const std::vector<View> &sm = src_in[path[jj - i + 1]];
+                        const std::vector<View> sm = src_at(jj - i + 1);
                         std::vector<int> u = vars, y;
                         for (const View &v : sm)
                             for (int w : v.vars)
@@ -1452,12 +1607,11 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                         fused = F;
                     }
                 }
-                if (fused) {
-                    jj -= fused;
-                } else {
-                    pi_step(jj);
-                    --jj;
-                }
+                const int pos = fused ? jj - fused + 1 : jj;      // the message just made: pi_pos
+                if (!fused) pi_step(jj);
+                jj = pos - 1;
+                // pi_pos's message in its own window's slicing (it was made in pos+1's)
+                if (have_pi && win[pos] != win[pos + 1]) pi_cur = xchg(pi_cur, pos, win[pos + 1], win[pos]);
             }
             pi_pos = std::min(pi_pos, j);
         };
@@ -1468,15 +1622,26 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             pi_down_to(j);
             std::vector<View> bel{lam_j};
             if (have_pi) bel.push_back(pi_cur);
+            const std::vector<int> &Sj = Sof(win[j]);          // conditioned away on this rank
+            std::vector<int> slow_j;
+            for (int v : slow[j])
+                if (!contains(Sj, v)) slow_j.push_back(v);
+            auto mark = [&](const std::vector<int> &ts) {
+                for (int t : ts) {
+                    auto it = std::find(Sj.begin(), Sj.end(), t);
+                    if (it != Sj.end()) slice_bit_of[t] = sbits - 1 - (int)(it - Sj.begin());
+                }
+            };
             auto mit = multi.find(j);
             if (mit != multi.end()) {
+                mark(mit->second);
                 int tb = -1;                                   // one pass: sum the slow vars
-                if (slow[j].size() >= 2) {
+                if (slow_j.size() >= 2) {
                     std::vector<View> mg = bel;
-                    int vv = B.merge_group(mg, slow[j]);
+                    int vv = B.merge_group(mg, slow_j);
                     if (vv >= 0) tb = B.emit(mg, vv, false);
                 } else {
-                    tb = B.emit(bel, slow[j].empty() ? -1 : slow[j][0], false);
+                    tb = B.emit(bel, slow_j.empty() ? -1 : slow_j[0], false);
                 }
                 if (tb >= 0 && !std::getenv("BNPP_NO_REDUCE_MANY")) {
                     B.reduce_many(B.view(tb), mit->second, result_of);
@@ -1486,8 +1651,10 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 }
             }
             auto dit = direct.find(j);
-            if (dit != direct.end())
+            if (dit != direct.end()) {
+                mark(dit->second);
                 for (int t : dit->second) result_of[t] = B.reduce_to(bel, t);
+            }
             --next_deliver;
             return true;
         };
@@ -1498,16 +1665,20 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             if (start) {
                 cur = *start;
             } else {                                   // the path's first bucket: no incoming message
-                cur = forward(path[k], nullptr);
+                cur = forward(k, nullptr);
                 ++k;
             }
             while (k <= to) {
+                // lam_{k-1} in bucket k's slicing; a run stays in one window
+                if (win[k] != win[k - 1]) cur = xchg(cur, k - 1, win[k - 1], win[k]);
+                int span = 1;
+                while (k + span <= to && win[k + span] == win[k]) ++span;
                 // longest fusable run of forward buckets k, k+1, ... (chain.cuh)
                 int fused = 0;
-                for (int F = chain_first_try(to - k + 1); F >= 2 && !fused; --F) {
-                    if ((to - k + 1) - F == 1 && F > 2) continue;   // never strand one bucket
+                for (int F = chain_first_try(span); F >= 2 && !fused; --F) {
+                    if (span - F == 1 && F > 2) continue;   // never strand one bucket
                     std::vector<PlanBuilder::ChainStep> steps;
-                    for (int i = 0; i < F; ++i) steps.push_back({src_in[path[k + i]], order[path[k + i]]});
+                    for (int i = 0; i < F; ++i) steps.push_back({src_at(k + i), order[path[k + i]]});
                     const int t = B.emit_chain(cur, steps);
                     if (t >= 0) {
                         cur = B.view(t);
@@ -1520,7 +1691,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                     if (std::getenv("BNPP_DEBUG_CHAIN"))
                         std::fprintf(stderr, "[chain] single forward bucket at %d (run %d..%d) vars %zu\n", k, from, to,
                                      cur.vars.size());
-                    cur = forward(path[k], &cur);
+                    cur = forward(k, &cur);
                     ++k;
                 }
             }
@@ -1528,7 +1699,6 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         };
         // reverse(lo, hi, start, spos, s): deliver D[hi-1] ... D[lo] (binomial
         // checkpointing over the deliveries); `start` = lam at spos < D[lo]
-        bool ok = true;
         std::function<void(int, int, const View *, int, int)> reverse = [&](int rlo, int rhi, const View *start,
                                                                              int spos, int sl) {
             const int len = rhi - rlo;
@@ -1554,12 +1724,12 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             reverse(0, (int)D.size(), sp >= 0 ? &start : nullptr, sp, slots);
         }
         if (!ok || next_deliver != -1) {
-            if (msg) *msg = "internal: checkpoint schedule out of order";
+            if (msg) *msg = fail_msg.empty() ? "internal: checkpoint schedule out of order" : fail_msg;
             return false;
         }
         if (a == 0) {                                          // the leaf: its own bucket and pi_0
             pi_down_to(0);
-            std::vector<View> bel = src_in[path[0]];
+            std::vector<View> bel = src_at(0);
             if (have_pi) bel.push_back(pi_cur);
             result_of[order[path[0]]] = reduce_to(bel, order[path[0]]);
         }
@@ -1570,6 +1740,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         p.results.push_back(r);
         p.results_vars.push_back(r >= 0 ? p.msgs[r - p.n_src].vars : std::vector<int>{});
         p.results_owned.push_back(in_range ? owned_var[t] : (part == 0));
+        p.results_slice_bit.push_back(r >= 0 ? slice_bit_of[t] : -1);
     }
     B.finish();
     out = std::move(p);
@@ -1762,6 +1933,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 };
                 mix((uint64_t)(uint32_t)b.elim_var);
                 mix((uint64_t)b.level);
+                mix((uint64_t)(b.xchg * 16 + b.xchg_mode));
                 mix(b.divide ? 1 : 0);
                 mix(b.out_vars.size());
                 for (int v : b.out_vars) mix((uint64_t)v);
@@ -1879,6 +2051,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
             s.plan_result_table.push_back(res[r] >= 0 ? remap(pi, res[r]) : -1);
             s.plan_result_vars.push_back(res_vars[r]);
             s.plan_result_owned.push_back(r < plans[pi]->results_owned.size() ? plans[pi]->results_owned[r] : 1);
+            s.plan_result_slice_bit.push_back(r < plans[pi]->results_slice_bit.size() ? plans[pi]->results_slice_bit[r] : -1);
         }
     }
     std::vector<std::vector<int>> born_at(n_levels + 2), dies_at(n_levels + 2);
@@ -1977,10 +2150,21 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     parallel_for((int64_t)items.size(), [&](int64_t idx) {
         Item &it = items[idx];
         BucketSpec b = *it.b;
-        b.simple = simplify && lvl_n[it.level] > 1 && b.chain_x.empty() && !b.divide &&
+        b.simple = simplify && lvl_n[it.level] > 1 && b.chain_x.empty() && !b.divide && !b.xchg &&
                    plans[it.plan]->msgs[b.out_table - s.n_src].size <= simple_max;
         for (View &v : b.in) v.table = remap(it.plan, v.table);
         b.out_table = remap(it.plan, b.out_table);
+        if (b.xchg) {                        // an exchange step: the executor's, no kernel descriptor
+            it.d = BucketDesc{};
+            it.d.n_in = (int)b.in.size();
+            for (int i = 0; i < it.d.n_in && i < kMaxDescIn; ++i) it.d.in_table[i] = b.in[i].table;
+            it.d.out_table = b.out_table;
+            it.d.k = b.xchg_blocks;
+            it.d.out_size = s.table_size[b.out_table];
+            it.key = kXchgKeyBase + b.xchg * 16 + b.xchg_mode;
+            it.ok = b.in.size() <= (size_t)kMaxDescIn;
+            return;
+        }
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
         it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf)
@@ -2042,6 +2226,10 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 std::fprintf(stderr, " slots:");
                 for (int q = 0; q < F; ++q) std::fprintf(stderr, " %lld/%lld", (long long)pl[2 * q], (long long)pl[2 * q + 1]);
                 std::fprintf(stderr, "\n");
+            } else if (dump && g.variant >= kXchgKeyBase) {
+                std::fprintf(stderr, "L%d xchg kind=%d mode=%d blocks=%d tables:%d->%d entries=%lld\n", g.level,
+                             (g.variant - kXchgKeyBase) / 16, (g.variant - kXchgKeyBase) % 16, d.k, d.in_table[0],
+                             d.out_table, (long long)d.out_size);
             } else if (dump) {
                 std::fprintf(stderr, "L%d n_in=%d k=%d tile=%dx%d big=%d bcls=%d tiles=%lld dims:", g.level, d.n_in, d.k,
                              d.v1, d.v2, d.big, d.big >= 0 ? d.bcls : 0, (long long)d.n_tiles);

@@ -74,7 +74,24 @@ struct BucketSpec {
     // runs in the level's one generic 1x1 launch (launch count, not bandwidth,
     // bounds such levels)
     bool simple = false;
+    // message-sliced runs (plan_bucket_tree_chain with n_slices > 1): one step
+    // of a message exchange between ranks, run by the executor, not a kernel
+    // variant -- kXchgSync: all-gather of each rank's scale exponent of in[0]
+    // into out (n_slices + 1 int64 words); kXchgPack: in[0] scaled to the common
+    // exponent (read from in[1]) into out, blocks of the destination ranks
+    // slowest (xchg_mode 0: in[0] already is, 1: they are in[0]'s fastest
+    // variables -- a transpose); kXchgComm: collective from in[0] to out
+    // (xchg_mode 0: all-to-all, 1: all-gather), out's blocks by source rank
+    // slowest; kXchgUnpack: out = in[0] with the source blocks moved from
+    // slowest to fastest (a transpose)
+    int xchg = 0;
+    int xchg_mode = 0;
+    int xchg_blocks = 1;
 };
+enum XchgKind { kXchgNone = 0, kXchgSync = 1, kXchgPack = 2, kXchgComm = 3, kXchgUnpack = 4 };
+// schedule group variant of an exchange step: kXchgKeyBase + kind * 16 + mode
+// (above every kernel variant key, bnpp_device.h)
+constexpr int kXchgKeyBase = 1 << 24;
 
 // Compile one bucket into a descriptor + dims-pool rows.  max_vec: 4 (fp32) / 2 (fp64).
 // Returns false (with msg) on an invalid shape.
@@ -114,6 +131,14 @@ struct VEPlan {
     double entries = 0;                 // sum over buckets of prod(card) over the union scope
     double elems_moved = 0;             // sum over buckets of (|inputs| + |output|): algorithmic traffic
     int width = 0;                      // largest bucket output width
+    // message slicing: ranks that share the messages (1: none), this plan's
+    // rank, and per result the rank bit that indexes it (-1: the result is a
+    // table over its target; else a scalar, the target being a slice
+    // variable whose value is that bit of the rank)
+    int n_slices = 1, slice_rank = 0;
+    std::vector<int> results_slice_bit;
+    int n_xchg = 0;                     // message exchanges (all-to-all / all-gather)
+    double xchg_elems = 0;              // entries this rank sends to other ranks
 };
 
 // canonical: lay messages out with variables sorted by elimination rank
@@ -147,9 +172,18 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
 // forward message) down to it, and checkpoints only inside it.  chain_eb > 0:
 // runs of consecutive buckets are fused into chain kernels for that element
 // size (bnpp_device.h, ChainForm).
+// n_slices = 2^b > 1: message slicing over n_slices ranks (this plan is rank
+// slice_rank's).  The chain is cut into windows in which b binary variables
+// stay in every separator; inside a window each rank holds the messages (and
+// computes the buckets) conditioned on those variables = the bits of its
+// rank, 1/n_slices of the work and memory; between windows a message is
+// re-sliced by one all-to-all (kXchg* steps), at the chain's ends
+// all-gathered or conditioned.  Every rank computes a partial (unnormalised)
+// marginal of every target: the marginals are the sum over ranks.
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
-                            int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb = 0);
+                            int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb = 0,
+                            int n_slices = 1, int slice_rank = 0);
 
 // Flattened, level-ordered launch schedule over one or more plans sharing the
 // same sources.  Tables: [0, n_src) sources, then every plan's messages.
@@ -191,6 +225,7 @@ struct Schedule {
     std::vector<int> plan_result_table;     // per plan (-1: constant 1)
     std::vector<std::vector<int>> plan_result_vars;
     std::vector<char> plan_result_owned;     // per result: 0 = another part computes it
+    std::vector<int> plan_result_slice_bit;  // per result: VEPlan::results_slice_bit (-1: none)
     int64_t arena_bytes = 0;
     double entries = 0;
     double elems_moved = 0;

@@ -172,12 +172,60 @@ int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Execut
     return 0;
 }
 
-int launch(Context &ctx, Executable &ex, hipStream_t stream) {
+// one exchange step of a sliced run (plan.hpp BucketSpec::xchg, xchg.hip)
+static int run_xchg(Context &ctx, Executable &ex, const Schedule::Group &g, hipStream_t stream, const XchgHooks *hooks) {
+    const Schedule &sc = ex.sched;
+    const BucketDesc &d = sc.descs[g.begin];
+    const int kind = (g.variant - kXchgKeyBase) / 16, mode = (g.variant - kXchgKeyBase) % 16, R = d.k;
+    const bool f32 = ex.dtype == kF32;
+    const int64_t eb = f32 ? 4 : 8;
+    const int in_t = d.in_table[0], out_t = d.out_table;
+    auto call = [&](int op, const void *send, void *recv, int64_t bytes) {
+        if (!hooks || !hooks->fn) return fail(ctx, hipErrorInvalidValue, "sliced run without a collective");
+        if (hooks->fn(hooks->user, op, send, recv, bytes, stream) != 0)
+            return fail(ctx, hipErrorUnknown, "the exchange collective failed");
+        return 0;
+    };
+    hipError_t err = hipSuccess;
+    switch (kind) {
+        case kXchgSync: {
+            err = launch_xchg_sync(f32, ex.d_meta, in_t, out_t, R, stream);
+            if (err != hipSuccess) break;
+            int64_t *x = static_cast<int64_t *>(ex.h_meta[out_t].ptr);
+            return call(0, x + R, x, 8);
+        }
+        case kXchgPack:
+            err = launch_xchg_pack(f32, ex.d_meta, in_t, d.in_table[1], out_t, R, mode, sc.table_size[out_t], stream);
+            break;
+        case kXchgComm: {
+            const int64_t n = sc.table_size[in_t];
+            int rc = mode == 0 ? call(1, ex.h_meta[in_t].ptr, ex.h_meta[out_t].ptr, n / R * eb)
+                               : call(0, ex.h_meta[in_t].ptr, ex.h_meta[out_t].ptr, n * eb);
+            if (rc) return rc;
+            err = launch_xchg_meta(ex.d_meta, in_t, out_t, stream);
+            break;
+        }
+        case kXchgUnpack:
+            err = launch_xchg_unpack(f32, ex.d_meta, in_t, out_t, R, sc.table_size[in_t], stream);
+            break;
+        default:
+            return fail(ctx, hipErrorInvalidValue, "unknown exchange step");
+    }
+    if (err != hipSuccess) return fail(ctx, err, "exchange step");
+    return 0;
+}
+
+int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks) {
     const Schedule &sc = ex.sched;
     hipError_t err = hipMemcpyAsync(ex.d_meta, ex.d_meta0, sizeof(TableMeta) * (size_t)sc.n_tables,
                                     hipMemcpyDeviceToDevice, stream);
     if (err != hipSuccess) return fail(ctx, err, "hipMemcpyAsync(meta reset)");
     for (const Schedule::Group &g : sc.groups) {
+        if (g.variant >= kXchgKeyBase) {
+            int rc = run_xchg(ctx, ex, g, stream, hooks);
+            if (rc) return rc;
+            continue;
+        }
         err = launch_level(ex.dtype == kF32, g.variant, ex.d_desc + g.begin, g.end - g.begin, ex.d_pool, ex.d_meta,
                            g.vblocks, g.small_elems, ctx.max_grid, stream);
         if (err != hipSuccess) return fail(ctx, err, "launch_level");
@@ -308,7 +356,7 @@ int launch_program(Context &ctx, Program &pg, hipStream_t stream) {
     (void)eb;
     for (size_t b = 0; b < pg.parts.size(); ++b) {
         Executable &ex = pg.parts[b];
-        int rc = launch(ctx, ex, stream);
+        int rc = launch(ctx, ex, stream, &pg.hooks);
         if (rc) return rc;
         if (ex.n_copies > 0) {
             hipError_t err = launch_copies(ex.d_copies, ex.n_copies, stream);

@@ -30,6 +30,17 @@ struct SingleArgs {
     int64_t pool[kMaxPool];
 };
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream);
+// message exchange steps of sliced runs (xchg.hip; plan.hpp BucketSpec::xchg)
+hipError_t launch_xchg_sync(bool f32, TableMeta *meta, int in_t, int x_t, int R, hipStream_t s);
+hipError_t launch_xchg_pack(bool f32, TableMeta *meta, int in_t, int x_t, int out_t, int R, int mode, int64_t n,
+                            hipStream_t s);
+hipError_t launch_xchg_unpack(bool f32, TableMeta *meta, int in_t, int out_t, int R, int64_t n, hipStream_t s);
+hipError_t launch_xchg_meta(TableMeta *meta, int in_t, int out_t, hipStream_t s);
+// the collective a sliced run's exchanges call (bnpp_collective_fn, include/bnpp.h)
+struct XchgHooks {
+    int (*fn)(void *user, int op, const void *send, void *recv, int64_t bytes, void *stream) = nullptr;
+    void *user = nullptr;
+};
 // loopy BP, one workgroup (bp.hip)
 hipError_t launch_sum_product(const BpArgs &a, hipStream_t stream);
 
@@ -106,12 +117,13 @@ struct Program {
     int64_t results_bytes = 0;
     std::vector<std::vector<int64_t>> res_off;    // per part, per plan: byte offset (-1: constant 1)
     std::vector<std::vector<int64_t>> res_size;   // per part, per plan: entries
+    XchgHooks hooks;                              // sliced runs: the ranks' collective
 };
 
 int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out);
 void free_sources(Context &ctx, DeviceSources &s);
 int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex, void *shared_arena = nullptr);
-int launch(Context &ctx, Executable &ex, hipStream_t stream);
+int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks = nullptr);
 // waits for `stream`, downloads result tables: values as stored (double) and the exp2 scale
 int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<std::vector<double>> &vals,
                   std::vector<int64_t> &exp2);

@@ -36,6 +36,10 @@ _P = C.c_void_p
 _I = C.c_int
 _IP = C.POINTER(C.c_int)
 _DP = C.POINTER(C.c_double)
+_LP = C.POINTER(C.c_int64)
+# bnpp_collective_fn (include/bnpp.h): (user, op, send, recv, bytes, stream) -> 0 on success
+COLLECTIVE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
+COLL_ALLGATHER, COLL_ALLTOALL = 0, 1
 
 _SIGS = {
     "bnpp_strerror": (C.c_char_p, [_I]),
@@ -70,6 +74,10 @@ _SIGS = {
     "bnpp_marginals_tree": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, _DP, _DP]),
     "bnpp_marginals_tree_part": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, _I, _I, _DP, _IP, _DP]),
     "bnpp_plan_tree_part": (_I, [_P, _I, _IP, _IP, _I, _IP, _I, _I, _I, _I, _IP, _DP, _I]),
+    "bnpp_marginals_tree_sliced": (_I, [_P, _P, _I, _IP, _IP, _I, _IP, _I, _I, _IP, _I, _I, COLLECTIVE_FN, _P,
+                                        C.c_double, _I, _DP, _LP, _DP]),
+    "bnpp_collective_loopback": (_I, [_P, _I, _P, _P, C.c_int64, _P]),
+    "bnpp_plan_tree_sliced": (_I, [_P, _I, _IP, _IP, _I, _IP, _I, _I, _I, _I, _IP, _DP, _I]),
     "bnpp_variable_elimination": (_I, [_P, _P, _I, _IP, _I, _I, _I, _IP, _IP, C.c_int64, C.POINTER(C.c_int64), _DP,
                                        C.POINTER(C.c_int64)]),
     "bnpp_plan_stats": (_I, [_P, _I, _I, _IP, _IP, _I, _IP, _I, _I, _DP, _I]),
@@ -88,7 +96,7 @@ EXPORTED = sorted(_SIGS)
 
 # The signature table above is for this ABI version (include/bnpp.h
 # BNPP_VERSION); a library of another version would take shifted arguments.
-ABI_VERSION = 200
+ABI_VERSION = 201
 if _lib.bnpp_version() != ABI_VERSION:
     raise ImportError("libbnpp.so ABI version %d, this binding expects %d (%s)"
                       % (_lib.bnpp_version(), ABI_VERSION, LIB_PATH))
@@ -342,6 +350,72 @@ def plan_tree_part(model: Model, part: int, n_parts: int, evidence=None, heurist
     _check(_lib.bnpp_plan_tree_part(model.handle, n, ev_v, ev_x, h, oa, len(order) if order is not None else 0,
                                     part, n_parts, dtype, owned, st, 8), "bnpp_plan_tree_part")
     return [v for v in range(model.n_vars) if owned[v]], list(st)
+
+
+NO_EXP = -(1 << 40)       # out_exp2 of an all-zero share (include/bnpp.h)
+
+
+def marginals_tree_sliced(ctx: Context, model: Model, rank: int, n_ranks: int, collective, evidence=None,
+                          heuristic: str = "mf", dtype: int = F32, targets: Optional[Sequence[int]] = None,
+                          order: Optional[Sequence[int]] = None, budget_gb: float = 0.0):
+    """This rank's share of the message-sliced bucket-tree marginals
+    (bnpp_marginals_tree_sliced) -> ({var: mantissas}, {var: exp2}, uptime_ms);
+    the marginal of v is the normalised sum over ranks of mantissas * 2^exp2
+    (bnpp.dist.sliced_tree_marginals).  collective: "loopback" (one GPU, a
+    world of identical ranks: timing only; "loopback-nocopy": no bytes move)
+    or callable(op, send, recv, nbytes,
+    stream) with op COLL_ALLGATHER / COLL_ALLTOALL and device addresses.
+    budget_gb > 0: the memory budget the plan must fit (every rank must pass
+    the same: it sets the checkpoint count); 0: this device's free memory."""
+    n, ev_v, ev_x = _ev(evidence)
+    tg = list(range(model.n_vars)) if targets is None else list(targets)
+    total = sum(model.cards[t] for t in tg)
+    out = (C.c_double * max(total, 1))()
+    exps = (C.c_int64 * max(len(tg), 1))()
+    up = C.c_double()
+    oa = _ints(list(order)) if order is not None else None
+    h = ORDER_GIVEN if order is not None else HEURISTICS[heuristic]
+    errors = []
+    user = None
+    if collective in ("loopback", "loopback-nocopy"):
+        fn = COLLECTIVE_FN(C.cast(_lib.bnpp_collective_loopback, C.c_void_p).value)
+        nr = (C.c_int * 2)(n_ranks, 1 if collective == "loopback-nocopy" else 0)
+        user = C.cast(nr, C.c_void_p)
+    else:
+        def _cb(_user, op, send, recv, nbytes, stream):
+            try:
+                collective(op, send, recv, nbytes, stream)
+                return 0
+            except BaseException as e:          # never unwind through the C frames
+                errors.append(e)
+                return 1
+        fn = COLLECTIVE_FN(_cb)
+    rc = _lib.bnpp_marginals_tree_sliced(ctx.handle, model.handle, n, ev_v, ev_x, h, oa,
+                                         len(order) if order is not None else 0, len(tg), _ints(tg), rank, n_ranks,
+                                         fn, user, C.c_double(budget_gb), dtype, out, exps, C.byref(up))
+    if errors:
+        raise errors[0]
+    _check(rc, "bnpp_marginals_tree_sliced")
+    mant, ex, o = {}, {}, 0
+    for i, t in enumerate(tg):
+        mant[t] = list(out[o:o + model.cards[t]])
+        ex[t] = exps[i]
+        o += model.cards[t]
+    return mant, ex, up.value
+
+
+def plan_tree_sliced(model: Model, rank: int, n_ranks: int, evidence=None, heuristic: str = "mf", dtype: int = F32,
+                     order: Optional[Sequence[int]] = None):
+    """Host-only plan of one rank of the sliced bucket tree -> (slice bit per
+    variable, stats: Job's 8 then [8] exchanges, [9] bytes sent per call)."""
+    n, ev_v, ev_x = _ev(evidence)
+    sb = (C.c_int * max(model.n_vars, 1))()
+    st = (C.c_double * 10)()
+    oa = _ints(list(order)) if order is not None else None
+    h = ORDER_GIVEN if order is not None else HEURISTICS[heuristic]
+    _check(_lib.bnpp_plan_tree_sliced(model.handle, n, ev_v, ev_x, h, oa, len(order) if order is not None else 0,
+                                      rank, n_ranks, dtype, sb, st, 10), "bnpp_plan_tree_sliced")
+    return list(sb)[:model.n_vars], list(st)
 
 
 def variable_elimination(ctx: Context, model: Model, variables: Sequence[int], heuristic: str = "given",

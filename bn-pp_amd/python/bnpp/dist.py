@@ -13,6 +13,12 @@ path shards without any data-path exchange:
     log-sum-exp give log10 Z.
   * One huge bucket: its output is split on leading variables (a view with the
     leading variable conditioned), i.e. the same cutset trick at bucket level.
+  * Sliced bucket-tree MAR (bnpp_marginals_tree_sliced): every message of a
+    chain-shaped tree is split over the ranks by log2(world) binary variables
+    that stay in the separators for a window of the chain; each rank computes
+    1/world of every bucket, and between windows one all-to-all re-slices the
+    message (sliced_tree_marginals).  This is the one path with a
+    data-path exchange.
 
 The compute is passed in as a callable so the same logic runs on the GPU
 engine (bench.py) and, in the CPU tests, against the oracle over gloo.
@@ -113,3 +119,132 @@ def _comm_device(dist):
     if backend == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
+
+
+class TorchCollective:
+    """bnpp_collective_fn over torch.distributed for a sliced run.
+
+    nccl (RCCL over xGMI): the engine's device buffers are wrapped as uint8
+    tensors (CUDA array interface) and the collective runs on the engine's
+    stream (ExternalStream), so RCCL orders itself after the pack kernel and
+    the next kernel after RCCL.  gloo (tests, CPU): the engine's stream is
+    synchronised, the bytes staged through host memory."""
+
+    def __init__(self, ctx, dist, world: int):
+        import bnpp
+        self.ctx, self.dist, self.world, self.bnpp = ctx, dist, world, bnpp
+        self.backend = dist.get_backend() if dist.is_initialized() else "gloo"
+        self.calls = 0
+        self.bytes_sent = 0
+
+    def _host(self, ptr: int, nbytes: int):
+        import numpy as np
+        import torch
+        buf = np.empty(nbytes, dtype=np.uint8)
+        self.bnpp._check(self.bnpp._lib.bnpp_memcpy_d2h(self.ctx.handle, buf.ctypes.data, ptr, nbytes), "d2h")
+        return torch.from_numpy(buf)
+
+    def _device(self, ptr: int, nbytes: int):
+        import torch
+
+        class _CAI:
+            pass
+        o = _CAI()
+        o.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3,
+                                      "strides": None}
+        return torch.as_tensor(o, device="cuda")
+
+    def __call__(self, op: int, send: int, recv: int, nbytes: int, stream: int):
+        import torch
+        import bnpp
+        self.calls += 1
+        R = self.world
+        self.bytes_sent += nbytes * (R - 1)
+        if self.backend == "nccl":
+            s = torch.cuda.ExternalStream(stream)
+            with torch.cuda.stream(s):
+                st = self._device(send, nbytes * (R if op == bnpp.COLL_ALLTOALL else 1))
+                rt = self._device(recv, nbytes * R)
+                if op == bnpp.COLL_ALLGATHER:
+                    self.dist.all_gather_into_tensor(rt, st)
+                else:
+                    self.dist.all_to_all_single(rt, st)
+            return
+        bnpp._check(bnpp._lib.bnpp_synchronize(self.ctx.handle, stream), "bnpp_synchronize")
+        st = self._host(send, nbytes * (R if op == bnpp.COLL_ALLTOALL else 1))
+        rt = torch.empty(nbytes * R, dtype=torch.uint8)
+        if op == bnpp.COLL_ALLGATHER:
+            self.dist.all_gather(list(rt.chunk(R)), st)
+        else:
+            self.dist.all_to_all_single(rt, st)
+        arr = rt.numpy()
+        bnpp._check(bnpp._lib.bnpp_memcpy_h2d(self.ctx.handle, recv, arr.ctypes.data, nbytes * R), "h2d")
+
+
+def combine_shares(n_vars: int, cards: Sequence[int], mant: Dict[int, List[float]], exps: Dict[int, int],
+                   dist=None) -> Dict[int, List[float]]:
+    """Sum every rank's share mantissa * 2^exp2 (one all_reduce(MAX) of the
+    exponents, one all_reduce(SUM) of the aligned fp64 shares) and normalise."""
+    import torch
+
+    offs = [0]
+    for c in cards:
+        offs.append(offs[-1] + c)
+    flat = torch.zeros(offs[-1], dtype=torch.float64)
+    ex = torch.full((n_vars,), -(1 << 40), dtype=torch.int64)
+    for t, e in exps.items():
+        ex[t] = e
+    multi = dist is not None and dist.is_initialized() and dist.get_world_size() > 1
+    if multi:
+        dev = _comm_device(dist)
+        eb = ex.to(dev)
+        dist.all_reduce(eb, op=dist.ReduceOp.MAX)
+        emax = eb.cpu()
+    else:
+        emax = ex
+    for t, vals in mant.items():
+        sh = int(max(min(exps[t] - int(emax[t]), 4000), -4000))
+        flat[offs[t]:offs[t] + cards[t]] = torch.tensor([math.ldexp(v, sh) for v in vals], dtype=torch.float64)
+    if multi:
+        buf = flat.to(_comm_device(dist))
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        flat = buf.cpu()
+    res = {}
+    for t in range(n_vars):
+        v = flat[offs[t]:offs[t + 1]]
+        z = float(v.sum())
+        res[t] = (v / z).tolist() if z > 0 else [1.0 / cards[t]] * cards[t]
+    return res
+
+
+def torch_min_budget_gb(dist) -> float:
+    """0.85 x the smallest free device memory over the ranks, in GB (0: the
+    engine's own choice, when no distributed world or no device is up)."""
+    import os
+    import torch
+    if os.environ.get("BNPP_MEM_BUDGET_GB"):
+        return float(os.environ["BNPP_MEM_BUDGET_GB"])
+    if not torch.cuda.is_available():
+        return 0.0
+    free = torch.tensor([float(torch.cuda.mem_get_info()[0])], dtype=torch.float64)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        buf = free.to(_comm_device(dist))
+        dist.all_reduce(buf, op=dist.ReduceOp.MIN)
+        free = buf.cpu()
+    return float(free[0]) * 0.85 / 1e9
+
+
+def sliced_tree_marginals(ctx, model, rank: int, world: int, dist=None, evidence=None, heuristic: str = "mf",
+                          dtype=None, order=None):
+    """Bucket-tree marginals with every message sliced over `world` ranks
+    (bnpp_marginals_tree_sliced): -> ({var: marginal}, collective stats)."""
+    import bnpp
+
+    coll = TorchCollective(ctx, dist, world)
+    # every rank must plan the same checkpoint count (the exchanges are
+    # collectives): the smallest free memory of the world sets the budget
+    budget = torch_min_budget_gb(dist)
+    mant, exps, up = bnpp.marginals_tree_sliced(ctx, model, rank, world, coll, evidence, heuristic,
+                                                bnpp.F32 if dtype is None else dtype, order=order, budget_gb=budget)
+    res = combine_shares(model.n_vars, model.cards, mant, exps, dist)
+    return res, {"calls": coll.calls, "bytes_sent": coll.bytes_sent, "uptime_ms": up}

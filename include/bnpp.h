@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BNPP_VERSION 200   /* 200: single ops take n_cards (the length of cards) */
+#define BNPP_VERSION 201   /* 200: single ops take n_cards (the length of cards); 201: sliced bucket-tree marginals */
 
 enum bnpp_status {
     BNPP_OK = 0,
@@ -188,6 +188,42 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
                              int heuristic, const int *order, int n_order, int n_targets, const int *targets,
                              int part, int n_parts, int dtype, double *out, int *owned, double *uptime_ms);
 
+/* Message-sliced bucket-tree marginals for multi-GPU runs (no reference
+ * counterpart: the reference is single-process; this replaces the N
+ * independent VEs of BN::marginals, model.cpp:303-346, across N ranks).  Every
+ * message of the chain-shaped bucket tree is split into n_ranks blocks by
+ * log2(n_ranks) binary variables that stay in the separators for a window of
+ * the chain; rank r holds and computes the block whose slice variables read r
+ * (slowest first), and between windows a message is re-sliced by one
+ * all-to-all through `coll` (at the chain's ends an all-gather).  n_ranks: a
+ * power of two >= 2; every rank calls this with the same model, evidence,
+ * order, targets and budget_gb (> 0: the device memory in GB the plan must
+ * fit, which sets its checkpoint count -- it must agree across ranks, e.g. the
+ * smallest free memory; <= 0: this device's).  The collective is called synchronously from this
+ * thread, in the same sequence on every rank, and must be complete (or
+ * enqueued on `stream`) when it returns:
+ *   op BNPP_COLL_ALLGATHER: each rank contributes `bytes` at send; recv gets
+ *                           rank r's at recv + r * bytes
+ *   op BNPP_COLL_ALLTOALL:  send holds n_ranks blocks of `bytes`, block d for
+ *                           rank d; recv gets rank s's block at recv + s * bytes
+ * Output: this rank's share of each target's unnormalised marginal, as
+ * mantissas (out, sum(card) doubles) times 2^out_exp2[i] per target
+ * (out_exp2 = -2^40 for an all-zero share); the marginal is the normalised sum
+ * of the shares over the ranks (bnpp.dist.sliced_tree_marginals).  Trees that
+ * are not chains, or chains without such windows: BNPP_ERR_UNSUPPORTED. */
+#define BNPP_COLL_ALLGATHER 0
+#define BNPP_COLL_ALLTOALL 1
+typedef int (*bnpp_collective_fn)(void *user, int op, const void *send, void *recv, int64_t bytes, void *stream);
+int bnpp_marginals_tree_sliced(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals,
+                               int heuristic, const int *order, int n_order, int n_targets, const int *targets,
+                               int rank, int n_ranks, bnpp_collective_fn coll, void *user, double budget_gb,
+                               int dtype, double *out, int64_t *out_exp2, double *uptime_ms);
+/* A collective for one GPU (user: const int[2] = {n_ranks, flags}): every
+ * received block is a copy of the sent one -- a world of identical ranks, for
+ * timing one rank's share of a sliced run (the data it computes is not a real
+ * world's); flags & 1: nothing is copied (the compute alone). */
+int bnpp_collective_loopback(void *user, int op, const void *send, void *recv, int64_t bytes, void *stream);
+
 /* BN::marginals with options["sum-product"] (model.cpp:313-317; the `bn -sp`
  * flag): loopy BP on the factor graph of the model's factors,
  * FactorGraph::update(max_iter, eps) (graph.cpp:298-332; the reference uses
@@ -222,6 +258,14 @@ int bnpp_plan_stats(const bnpp_model *m, int kind, int n_ev, const int *ev_vars,
 int bnpp_plan_tree_part(const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
                         const int *order, int n_order, int part, int n_parts, int dtype, int *owned, double *stats,
                         int n_stats);
+
+/* Host-only planning of one rank of bnpp_marginals_tree_sliced (all
+ * variables as targets): slice_bit[v] (may be NULL) = the rank bit that
+ * indexes v's scalar share (-1: a table over v); stats as bnpp_job_stats, then
+ * [8] message exchanges, [9] bytes this rank sends per call. */
+int bnpp_plan_tree_sliced(const bnpp_model *m, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
+                          const int *order, int n_order, int rank, int n_ranks, int dtype, int *slice_bit,
+                          double *stats, int n_stats);
 
 /* ------------------------------------------- prepared jobs (benchmark) */
 /* A planned, device-resident inference that can be launched repeatedly. */

@@ -368,3 +368,30 @@ def test_plan_stats_saturate_on_infeasible_widths():
     with pytest.raises(bnpp.BnppError) as e:
         bnpp.plan_stats(p, 0, {}, "mf", dtype=bnpp.F32)
     assert e.value.status == bnpp.ERR_OOM
+
+
+def test_plan_tree_sliced_shares_work_and_exchanges():
+    """Message slicing (bnpp_plan_tree_sliced): every rank plans the same
+    schedule (buckets, levels, exchanges, bytes) on 1/R of each message, so a
+    rank's factor-entries fall ~1/R (below 1/R against the checkpointed one-rank
+    tree: the sliced plan keeps every forward message); slice bits index the
+    rank's log2(R) bits."""
+    r = c = 16
+    m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=0))
+    col = [i * c + j for j in range(c) for i in range(r)]
+    full = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+    per = []
+    for R in (2, 4, 8):
+        plans = [bnpp.plan_tree_sliced(m, k, R, order=col) for k in range(R)]
+        st0 = plans[0][1]
+        for sb, st in plans:
+            assert st[2:4] == st0[2:4] and st[8:10] == st0[8:10]
+            assert all(-1 <= b < R.bit_length() - 1 for b in sb)
+        assert st0[8] > 0 and st0[9] > 0
+        per.append(st0[0])
+    assert per[0] < 0.6 * full[0]
+    assert per[2] < per[1] < per[0]
+    with pytest.raises(bnpp.BnppError):
+        bnpp.plan_tree_sliced(m, 0, 3, order=col)              # not a power of two
+    with pytest.raises(bnpp.BnppError):
+        bnpp.plan_tree_sliced(bnpp.Model.load(model_path("alarm.uai")), 0, 2)   # not a chain
