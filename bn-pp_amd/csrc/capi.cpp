@@ -272,6 +272,20 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             // (chain-shaped trees), with as many checkpoint slots as fit
             std::string msg;
             VEPlan best;
+            // sliced runs: the two-front schedule (two concurrent lanes, no
+            // recomputation) when its arena fits, else checkpointing on one lane
+            if (n_slices > 1 && !(std::getenv("BNPP_SLICE_LANES") && *std::getenv("BNPP_SLICE_LANES") == '0')) {
+                VEPlan cp;
+                if (plan_bucket_tree_chain(d.cards, views, ord, targets, 1, part, n_parts, cp, &msg, chain_eb, n_slices,
+                                           slice_rank, true)) {
+                    if (need(cp) <= budget) {
+                        plans.back() = std::move(cp);
+                        return BNPP_OK;
+                    }
+                } else {
+                    return set_err(BNPP_ERR_UNSUPPORTED, msg);
+                }
+            }
             // sliced messages are 1/n_slices of the size: room for more checkpoints
             int lo = 1, hi = n_slices > 1 ? 256 : 64, best_s = 0;
             const uint64_t key = slot_key(d.cards, scopes, ord, targets, eb, chain_eb, part, n_parts, n_slices);
@@ -685,6 +699,7 @@ int bnpp_ctx_destroy(bnpp_ctx *ctx) {
     if (!ctx) return BNPP_OK;
     (void)hipSetDevice(ctx->c.device);
     if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
+    if (ctx->c.lane_stream) (void)hipStreamDestroy(ctx->c.lane_stream);
     drop_arena_cache(ctx->c);
     drop_buffer_cache(ctx->c);
     delete ctx;
@@ -1193,15 +1208,23 @@ int bnpp_marginals_tree_sliced(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, con
     BNPP_GUARD_END
 }
 
-// a world of n_ranks identical ranks (user: int[2] = {n_ranks, flags}):
-// every block this rank would receive is a copy of what it sends -- the
-// timing of one rank's share of a sliced run on one GPU, the data movement
-// local; flags & 1: no bytes move (the exchanges' transfer time left out)
+// a world of n_ranks identical ranks (user: int[4] = {n_ranks, flags,
+// link MB/s, latency us}): every block this rank would receive is a copy of
+// what it sends -- the timing of one rank's share of a sliced run on one GPU,
+// the data movement local; flags & 1: no bytes move; flags & 2: the stream
+// waits the transfer's modelled xGMI time (latency + bytes sent over
+// min(n_ranks - 1, 7) links at the given rate each)
 int bnpp_collective_loopback(void *user, int op, const void *send, void *recv, int64_t bytes, void *stream) {
     if (!user || !send || !recv || bytes < 0) return 1;
-    const int R = static_cast<const int *>(user)[0];
-    if (static_cast<const int *>(user)[1] & 1) return 0;    // no data movement: the compute alone
+    const int *u = static_cast<const int *>(user);
+    const int R = u[0];
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (u[1] & 2) {                                          // a modelled transfer: the stream waits its duration
+        const double links = R - 1 < 7 ? R - 1 : 7, sent = (double)bytes * (R - 1);
+        const double ns = u[3] * 1e3 + sent / (links * (double)u[2] * 1e6) * 1e9;
+        if (launch_delay(ns, s) != hipSuccess) return 1;
+    }
+    if (u[1] & 1) return 0;                                  // no data movement: the compute alone
     if (op == BNPP_COLL_ALLGATHER) {
         for (int r = 0; r < R; ++r)
             if (hipMemcpyAsync(static_cast<char *>(recv) + (int64_t)r * bytes, send, (size_t)bytes,

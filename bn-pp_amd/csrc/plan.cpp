@@ -798,6 +798,7 @@ struct PlanBuilder {
     std::vector<int> level;                 // per table
     bool sequential = false;                // every bucket one level after the previous (program order)
     int last_level = 0;
+    int lane = 0;                           // BucketSpec::lane of the buckets emitted now
 
     PlanBuilder(const std::vector<int> &c, VEPlan &plan, const std::vector<View> &sources,
                 const std::vector<int> &order, bool canon_layout)
@@ -840,6 +841,7 @@ struct PlanBuilder {
     }
     int push_bucket(const std::vector<View> &in, int x, const std::vector<int> &ov, bool free_level = false) {
         BucketSpec b;
+        b.lane = lane;
         b.in = in;
         b.elim_var = x;
         b.out_vars = ov;
@@ -858,6 +860,7 @@ struct PlanBuilder {
     // traffic counted (the sync step's few bytes are not)
     int push_xchg(const std::vector<View> &in, const std::vector<int> &ov, int kind, int mode, int blocks) {
         BucketSpec b;
+        b.lane = lane;
         b.in = in;
         b.elim_var = -1;
         b.out_vars = ov;
@@ -938,6 +941,7 @@ struct PlanBuilder {
             vars = remove_var(u, st.x);
         }
         BucketSpec b;
+        b.lane = lane;
         b.in.push_back(big);
         b.out_vars = canon(vars);
         b.chain_x = xs;
@@ -1284,7 +1288,7 @@ int64_t binom_capped(int n, int k) {             // C(n, k), saturating at 2^40
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
                             int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb, int n_slices,
-                            int slice_rank) {
+                            int slice_rank, bool lanes) {
     if (n_parts < 1 || part < 0 || part >= n_parts) {
         if (msg) *msg = "bad part";
         return false;
@@ -1381,6 +1385,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         off += m;
         if (a >= b) continue;
         for (int q = a; q < b; ++q) owned_var[order[path[q]]] = 1;
+        B.lane = 0;
         // ---- message slicing (n_slices > 1) ----
         // windows: win[j] = the window of position j (-1: every rank holds the
         // whole message), Sw[k] its slice variables (canonical order; S[i]'s
@@ -1616,12 +1621,8 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             pi_pos = std::min(pi_pos, j);
         };
         int next_deliver = (int)D.size() - 1;
-        auto deliver = [&](int i, const View &lam_j) {
-            if (i != next_deliver) return false;
-            const int j = D[i];
-            pi_down_to(j);
-            std::vector<View> bel{lam_j};
-            if (have_pi) bel.push_back(pi_cur);
+        // the marginals delivered at position j from its belief (lam_j, pi_j)
+        auto deliver_bel = [&](int j, const std::vector<View> &bel) {
             const std::vector<int> &Sj = Sof(win[j]);          // conditioned away on this rank
             std::vector<int> slow_j;
             for (int v : slow[j])
@@ -1655,6 +1656,14 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 mark(dit->second);
                 for (int t : dit->second) result_of[t] = B.reduce_to(bel, t);
             }
+        };
+        auto deliver = [&](int i, const View &lam_j) {
+            if (i != next_deliver) return false;
+            const int j = D[i];
+            pi_down_to(j);
+            std::vector<View> bel{lam_j};
+            if (have_pi) bel.push_back(pi_cur);
+            deliver_bel(j, bel);
             --next_deliver;
             return true;
         };
@@ -1717,7 +1726,54 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             ok = ok && deliver(c, ck);
             reverse(rlo, c, start, spos, sl);
         };
-        if (!D.empty()) {
+        if (lanes && !D.empty()) {
+            // Two fronts, no recomputation: lane 0 streams the forward messages
+            // up the chain, lane 1 the backward messages down it, concurrently
+            // (the executor runs the lanes on two streams, so one lane's
+            // exchanges overlap the other's buckets).  At a delivery position
+            // the front that arrives first (fewer buckets from its end) keeps
+            // its message; the second one forms the belief and delivers.
+            struct Ev { int dist, lane, i; };
+            std::vector<Ev> evs;
+            for (int i = 0; i < (int)D.size(); ++i) {
+                evs.push_back({D[i] + 1, 0, i});
+                evs.push_back({m - 1 - D[i], 1, i});
+            }
+            std::sort(evs.begin(), evs.end(), [](const Ev &x, const Ev &y) {
+                return x.dist != y.dist ? x.dist < y.dist : x.lane > y.lane;
+            });
+            std::vector<char> seen(D.size(), 0);
+            std::vector<View> lam_kept(D.size()), pi_kept(D.size());
+            std::vector<char> pi_kept_has(D.size(), 0);
+            View lam_cur;
+            int lam_pos = -1;
+            const bool dbg = std::getenv("BNPP_DEBUG_LANES") != nullptr;
+            for (const Ev &e : evs) {
+                const int j = D[e.i];
+                if (dbg) std::fprintf(stderr, "[lanes] lane %d pos %d dist %d (lam_pos %d pi_pos %d)\n", e.lane, j, e.dist, lam_pos, pi_pos);
+                B.lane = e.lane;
+                if (e.lane == 0) {
+                    lam_cur = advance(lam_pos >= 0 ? &lam_cur : nullptr, lam_pos, j);
+                    lam_pos = j;
+                } else {
+                    pi_down_to(j);
+                }
+                if (!seen[e.i]) {                              // first arrival: keep this front's message
+                    seen[e.i] = 1;
+                    if (e.lane == 0) lam_kept[e.i] = lam_cur;
+                    else {
+                        pi_kept[e.i] = pi_cur;
+                        pi_kept_has[e.i] = have_pi;
+                    }
+                    continue;
+                }
+                std::vector<View> bel{e.lane == 0 ? lam_cur : lam_kept[e.i]};
+                if (e.lane == 0 ? pi_kept_has[e.i] : have_pi) bel.push_back(e.lane == 0 ? pi_kept[e.i] : pi_cur);
+                deliver_bel(j, bel);
+            }
+            B.lane = 1;
+            next_deliver = -1;
+        } else if (!D.empty()) {
             View start;                                        // prefix: stream to D[0] - 1, kept throughout
             const int sp = D[0] - 1;
             if (sp >= 0) start = advance(nullptr, -1, sp);
@@ -2039,6 +2095,27 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
             }
         }
     });
+    // lanes (sliced two-front schedules): a table is placed in its producer's
+    // lane's arena; one read by another lane is kept to the end (the lanes
+    // run concurrently, so a later level of the producer's lane may not
+    // reuse memory the other lane has yet to read)
+    std::vector<int> lane_of(s.n_tables, 0);
+    int n_lanes = 1;
+    for (size_t pi = 0; pi < plans.size(); ++pi)
+        for (const BucketSpec &b : plans[pi]->buckets) {
+            if (!kept(pi, b)) continue;
+            lane_of[remap(pi, b.out_table)] = b.lane;
+            n_lanes = std::max(n_lanes, b.lane + 1);
+        }
+    if (n_lanes > 1)
+        for (size_t pi = 0; pi < plans.size(); ++pi)
+            for (const BucketSpec &b : plans[pi]->buckets) {
+                if (!kept(pi, b)) continue;
+                for (const View &v : b.in) {
+                    const int t = remap(pi, v.table);
+                    if (t >= s.n_src && lane_of[t] != b.lane) last[t] = kForever;
+                }
+            }
     for (size_t pi = 0; pi < plans.size(); ++pi) {
         std::vector<int> res = plans[pi]->results;
         std::vector<std::vector<int>> res_vars = plans[pi]->results_vars;
@@ -2107,17 +2184,29 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         }
     }
     if (!placed) {
-        Arena arena;
+        std::vector<Arena> arenas(n_lanes);
         for (int L = 1; L <= n_levels; ++L) {
-            for (int t : born_at[L]) s.table_offset[t] = arena.alloc(sat_mul(s.table_size[t], elem_bytes));
-            for (int t : dies_at[L]) arena.release(s.table_offset[t], sat_mul(s.table_size[t], elem_bytes));
+            for (int t : born_at[L]) s.table_offset[t] = arenas[lane_of[t]].alloc(sat_mul(s.table_size[t], elem_bytes));
+            for (int t : dies_at[L]) arenas[lane_of[t]].release(s.table_offset[t], sat_mul(s.table_size[t], elem_bytes));
         }
-        s.arena_bytes = arena.top;
-        if (arena.saturated) {               // tables of 2^58+ bytes: no descriptors for those
+        int64_t base = 0;
+        bool sat = false;
+        std::vector<int64_t> lane_base(n_lanes, 0);
+        for (int l = 0; l < n_lanes; ++l) {
+            lane_base[l] = base;
+            base = sat_add(base, arenas[l].top);
+            sat = sat || arenas[l].saturated;
+        }
+        if (n_lanes > 1)
+            for (int t = s.n_src; t < s.n_tables; ++t)
+                if (canon[t] == t && s.table_offset[t] >= 0) s.table_offset[t] += lane_base[lane_of[t]];
+        s.arena_bytes = base;
+        if (sat) {                           // tables of 2^58+ bytes: no descriptors for those
             if (msg) *msg = "the plan's tables exceed any device (more than 2^58 bytes); use a narrower elimination order";
             return false;
         }
     }
+    s.n_lanes = n_lanes;
     for (int t = s.n_src; t < s.n_tables; ++t)
         if (canon[t] != t) s.table_offset[t] = s.table_offset[canon[t]];
     const double T1 = clk();
@@ -2182,7 +2271,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     // order by (level, variant), ties by item index (stable), on compact keys
     std::vector<std::pair<uint64_t, int>> sk(items.size());
     for (size_t i = 0; i < items.size(); ++i)
-        sk[i] = {((uint64_t)(uint32_t)items[i].level << 32) | (uint32_t)items[i].key, (int)i};
+        sk[i] = {((uint64_t)(uint32_t)items[i].level << 32) | ((uint64_t)items[i].b->lane << 28) | (uint32_t)items[i].key,
+                 (int)i};
     std::sort(sk.begin(), sk.end());
     std::vector<int> ord(items.size());
     std::vector<int64_t> pool_at(items.size() + 1, 0);
@@ -2201,9 +2291,11 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     const bool dump = std::getenv("BNPP_DUMP_PLAN") != nullptr;
     for (size_t i = 0; i < ord.size();) {
         const Item &first = items[ord[i]];
-        Schedule::Group g{first.level, first.key, (int)i, 0, 0, 0};
+        Schedule::Group g{first.level, first.key, (int)i, 0, 0, 0, first.b->lane};
         int64_t vb = 0;
-        for (; i < ord.size() && items[ord[i]].level == g.level && items[ord[i]].key == g.variant; ++i) {
+        for (; i < ord.size() && items[ord[i]].level == g.level && items[ord[i]].key == g.variant &&
+               items[ord[i]].b->lane == g.lane;
+             ++i) {
             const Item &it = items[ord[i]];
             BucketDesc &d = s.descs[i];
             d.vblk_begin = vb;

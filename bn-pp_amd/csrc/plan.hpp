@@ -87,6 +87,10 @@ struct BucketSpec {
     int xchg = 0;
     int xchg_mode = 0;
     int xchg_blocks = 1;
+    // stream lane (sliced two-front schedules: 0 forward messages, 1 backward
+    // messages and deliveries): lanes run concurrently, ordered by the
+    // cross-lane table dependencies only
+    int lane = 0;
 };
 enum XchgKind { kXchgNone = 0, kXchgSync = 1, kXchgPack = 2, kXchgComm = 3, kXchgUnpack = 4 };
 // schedule group variant of an exchange step: kXchgKeyBase + kind * 16 + mode
@@ -179,11 +183,13 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
 // rank, 1/n_slices of the work and memory; between windows a message is
 // re-sliced by one all-to-all (kXchg* steps), at the chain's ends
 // all-gathered or conditioned.  Every rank computes a partial (unnormalised)
-// marginal of every target: the marginals are the sum over ranks.
+// marginal of every target: the marginals are the sum over ranks.  lanes:
+// the two-front schedule (forward and backward messages on two concurrent
+// lanes, no recomputation; `slots` unused), else binomial checkpointing.
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
                             int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb = 0,
-                            int n_slices = 1, int slice_rank = 0);
+                            int n_slices = 1, int slice_rank = 0, bool lanes = false);
 
 // Flattened, level-ordered launch schedule over one or more plans sharing the
 // same sources.  Tables: [0, n_src) sources, then every plan's messages.
@@ -219,6 +225,7 @@ struct Schedule {
         int level, variant, begin, end;
         int64_t vblocks;
         int small_elems;                    // stream kernels: LDS elements for small inputs
+        int lane;                           // BucketSpec::lane (all buckets of a group share it)
     };
     std::vector<Group> groups;
     int n_levels = 0;
@@ -230,6 +237,7 @@ struct Schedule {
     double entries = 0;
     double elems_moved = 0;
     int width = 0;
+    int n_lanes = 1;                        // concurrent stream lanes (Group::lane)
 };
 
 // Peak bytes of live messages when the plan runs level by level (arena estimate).

@@ -169,6 +169,36 @@ int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Execut
     if (!sc.pool.empty() && (err = hipMemcpy(ex.d_pool, sc.pool.data(), sizeof(int64_t) * sc.pool.size(),
                                              hipMemcpyHostToDevice)) != hipSuccess)
         return fail(ctx, err, "hipMemcpy(pool)");
+    if (sc.n_lanes > 1) {
+        if (sc.n_lanes > 2) return fail(ctx, hipErrorInvalidValue, "more than two lanes");
+        if (!ctx.lane_stream && (err = hipStreamCreateWithFlags(&ctx.lane_stream, hipStreamNonBlocking)) != hipSuccess)
+            return fail(ctx, err, "hipStreamCreate(lane)");
+        // producer group of every table; a group consuming a table made on the
+        // other lane waits for the producer's event
+        std::vector<int> prod(sc.n_tables, -1);
+        const int ng = (int)sc.groups.size();
+        ex.g_record.assign(ng, -1);
+        ex.g_wait.assign(ng, {});
+        int n_ev = 2;
+        for (int gi = 0; gi < ng; ++gi) {
+            const Schedule::Group &g = sc.groups[gi];
+            for (int k = g.begin; k < g.end; ++k) {
+                const BucketDesc &d = sc.descs[k];
+                for (int i = 0; i < d.n_in && i < kMaxDescIn; ++i) {
+                    const int t = d.in_table[i], pg = t >= 0 ? prod[t] : -1;
+                    if (pg < 0 || sc.groups[pg].lane == g.lane) continue;
+                    if (ex.g_record[pg] < 0) ex.g_record[pg] = n_ev++;
+                    std::vector<int> &w = ex.g_wait[gi];
+                    if (std::find(w.begin(), w.end(), ex.g_record[pg]) == w.end()) w.push_back(ex.g_record[pg]);
+                }
+            }
+            for (int k = g.begin; k < g.end; ++k) prod[sc.descs[k].out_table] = gi;
+        }
+        ex.events.assign(n_ev, nullptr);
+        for (hipEvent_t &e : ex.events)
+            if ((err = hipEventCreateWithFlags(&e, hipEventDisableTiming)) != hipSuccess)
+                return fail(ctx, err, "hipEventCreate");
+    }
     return 0;
 }
 
@@ -220,16 +250,31 @@ int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *ho
     hipError_t err = hipMemcpyAsync(ex.d_meta, ex.d_meta0, sizeof(TableMeta) * (size_t)sc.n_tables,
                                     hipMemcpyDeviceToDevice, stream);
     if (err != hipSuccess) return fail(ctx, err, "hipMemcpyAsync(meta reset)");
-    for (const Schedule::Group &g : sc.groups) {
+    const bool lanes = sc.n_lanes > 1 && !ex.events.empty();
+    hipStream_t ls[2] = {stream, lanes ? ctx.lane_stream : stream};
+    if (lanes && ((err = hipEventRecord(ex.events[0], stream)) != hipSuccess ||
+                  (err = hipStreamWaitEvent(ls[1], ex.events[0], 0)) != hipSuccess))
+        return fail(ctx, err, "lane start");
+    for (size_t gi = 0; gi < sc.groups.size(); ++gi) {
+        const Schedule::Group &g = sc.groups[gi];
+        hipStream_t st = ls[lanes ? g.lane & 1 : 0];
+        if (lanes)
+            for (int e : ex.g_wait[gi])
+                if ((err = hipStreamWaitEvent(st, ex.events[e], 0)) != hipSuccess) return fail(ctx, err, "lane wait");
         if (g.variant >= kXchgKeyBase) {
-            int rc = run_xchg(ctx, ex, g, stream, hooks);
+            int rc = run_xchg(ctx, ex, g, st, hooks);
             if (rc) return rc;
-            continue;
+        } else {
+            err = launch_level(ex.dtype == kF32, g.variant, ex.d_desc + g.begin, g.end - g.begin, ex.d_pool, ex.d_meta,
+                               g.vblocks, g.small_elems, ctx.max_grid, st);
+            if (err != hipSuccess) return fail(ctx, err, "launch_level");
         }
-        err = launch_level(ex.dtype == kF32, g.variant, ex.d_desc + g.begin, g.end - g.begin, ex.d_pool, ex.d_meta,
-                           g.vblocks, g.small_elems, ctx.max_grid, stream);
-        if (err != hipSuccess) return fail(ctx, err, "launch_level");
+        if (lanes && ex.g_record[gi] >= 0 && (err = hipEventRecord(ex.events[ex.g_record[gi]], st)) != hipSuccess)
+            return fail(ctx, err, "lane record");
     }
+    if (lanes && ((err = hipEventRecord(ex.events[1], ls[1])) != hipSuccess ||
+                  (err = hipStreamWaitEvent(stream, ex.events[1], 0)) != hipSuccess))
+        return fail(ctx, err, "lane join");
     return 0;
 }
 
@@ -270,6 +315,8 @@ int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<
 }
 
 void free_executable(Context &ctx, Executable &ex) {
+    for (hipEvent_t e : ex.events)
+        if (e) (void)hipEventDestroy(e);
     if (ex.arena && ex.own_arena) (void)hipFree(ex.arena);
     put_buffer(ctx, ex.d_meta, ex.cap_meta);
     put_buffer(ctx, ex.d_meta0, ex.cap_meta0);

@@ -36,6 +36,8 @@ hipError_t launch_xchg_pack(bool f32, TableMeta *meta, int in_t, int x_t, int ou
                             hipStream_t s);
 hipError_t launch_xchg_unpack(bool f32, TableMeta *meta, int in_t, int out_t, int R, int64_t n, hipStream_t s);
 hipError_t launch_xchg_meta(TableMeta *meta, int in_t, int out_t, hipStream_t s);
+// stream `s` waits `ns` nanoseconds on the device (one sleeping wave)
+hipError_t launch_delay(double ns, hipStream_t s);
 // the collective a sliced run's exchanges call (bnpp_collective_fn, include/bnpp.h)
 struct XchgHooks {
     int (*fn)(void *user, int op, const void *send, void *recv, int64_t bytes, void *stream) = nullptr;
@@ -62,6 +64,8 @@ struct Context {
     std::mutex buf_mu;
     std::vector<std::pair<void *, size_t>> buf_free;   // (buffer, capacity)
     size_t buf_free_bytes = 0;
+    // the second lane of two-front schedules (Schedule::n_lanes), made on first use
+    hipStream_t lane_stream = nullptr;
 };
 
 // a device buffer of at least `bytes` from the context's cache (or hipMalloc);
@@ -100,6 +104,12 @@ struct Executable {
     std::vector<TableMeta> h_meta;
     CopyItem *d_copies = nullptr;       // result tables -> the program's results buffer
     int n_copies = 0;
+    // lanes: events a group records (-1: none) and the events it waits for
+    // (producers of its inputs on the other lane); events[0] starts lane 1
+    // after the metadata reset, events[1] joins it back before the results
+    std::vector<hipEvent_t> events;
+    std::vector<int> g_record;
+    std::vector<std::vector<int>> g_wait;
     size_t cap_meta = 0, cap_meta0 = 0, cap_desc = 0, cap_pool = 0, cap_copies = 0;   // buffer capacities
 };
 

@@ -116,6 +116,16 @@ __global__ void xchg_meta_kernel(TableMeta *__restrict__ meta, int in_t, int out
     }
 }
 
+// one wave sleeping on the device clock for `ticks`: the stream it is on
+// waits that long while other streams' kernels run (the loopback collective's
+// stand-in for a transfer's duration)
+__global__ void delay_kernel(uint64_t ticks) {
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = wall_clock64();
+        while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+    }
+}
+
 unsigned grid_for(int64_t work) {
     const int64_t g = (work + 255) / 256;
     return (unsigned)(g < 1 ? 1 : g > 16384 ? 16384 : g);
@@ -166,4 +176,19 @@ hipError_t launch_xchg_meta(TableMeta *meta, int in_t, int out_t, hipStream_t s)
     return hipGetLastError();
 }
 
+}  // namespace bnpp
+
+namespace bnpp {
+hipError_t launch_delay(double ns, hipStream_t s) {
+    static int khz = 0;
+    if (khz <= 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+            khz <= 0)
+            khz = 100000;                                  // 100 MHz, the gfx9 constant clock
+    }
+    const uint64_t ticks = (uint64_t)(ns * 1e-6 * khz);
+    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, ticks);
+    return hipGetLastError();
+}
 }  // namespace bnpp

@@ -377,9 +377,15 @@ def marginals_tree_sliced(ctx: Context, model: Model, rank: int, n_ranks: int, c
     h = ORDER_GIVEN if order is not None else HEURISTICS[heuristic]
     errors = []
     user = None
-    if collective in ("loopback", "loopback-nocopy"):
+    if isinstance(collective, str) and collective.startswith("loopback"):
+        # "loopback" (copies), "loopback-nocopy", "loopback-model:<MB/s per link>:<latency us>"
+        # (no copies; each exchange's stream waits the modelled xGMI time)
         fn = COLLECTIVE_FN(C.cast(_lib.bnpp_collective_loopback, C.c_void_p).value)
-        nr = (C.c_int * 2)(n_ranks, 1 if collective == "loopback-nocopy" else 0)
+        if collective.startswith("loopback-model"):
+            _, rate, lat = collective.split(":")
+            nr = (C.c_int * 4)(n_ranks, 3, int(rate), int(lat))
+        else:
+            nr = (C.c_int * 4)(n_ranks, 1 if collective == "loopback-nocopy" else 0, 0, 0)
         user = C.cast(nr, C.c_void_p)
     else:
         def _cb(_user, op, send, recv, nbytes, stream):

@@ -218,10 +218,12 @@ int bnpp_marginals_tree_sliced(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, con
                                int heuristic, const int *order, int n_order, int n_targets, const int *targets,
                                int rank, int n_ranks, bnpp_collective_fn coll, void *user, double budget_gb,
                                int dtype, double *out, int64_t *out_exp2, double *uptime_ms);
-/* A collective for one GPU (user: const int[2] = {n_ranks, flags}): every
- * received block is a copy of the sent one -- a world of identical ranks, for
- * timing one rank's share of a sliced run (the data it computes is not a real
- * world's); flags & 1: nothing is copied (the compute alone). */
+/* A collective for one GPU (user: const int[4] = {n_ranks, flags, link MB/s,
+ * latency us}): every received block is a copy of the sent one -- a world of
+ * identical ranks, for timing one rank's share of a sliced run (the data it
+ * computes is not a real world's); flags & 1: nothing is copied (the compute
+ * alone); flags & 2: the calling stream waits the transfer's modelled time,
+ * latency + bytes sent / (min(n_ranks - 1, 7) links x MB/s). */
 int bnpp_collective_loopback(void *user, int op, const void *send, void *recv, int64_t bytes, void *stream);
 
 /* BN::marginals with options["sum-product"] (model.cpp:313-317; the `bn -sp`

@@ -112,3 +112,32 @@ def test_sliced_requires_a_chain(ctx):
     with pytest.raises(bnpp.BnppError) as e:
         bnpp.marginals_tree_sliced(ctx, m, 0, 2, "loopback")
     assert e.value.status in (bnpp.ERR_UNSUPPORTED, bnpp.ERR_OOM)
+
+
+def test_torch_collective_wraps_engine_buffers(ctx):
+    """The RCCL path of bnpp.dist.TorchCollective hands the engine's device
+    buffers to torch.distributed as uint8 tensors (CUDA array interface):
+    the wrapped tensor aliases the engine's bytes both ways."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    from bnpp import dist as bdist
+
+    n = 4096
+    p = C.c_void_p()
+    bnpp._check(bnpp._lib.bnpp_malloc(ctx.handle, n, C.byref(p)), "malloc")
+    try:
+        src = (np.arange(n) % 251).astype(np.uint8)
+        bnpp._check(bnpp._lib.bnpp_memcpy_h2d(ctx.handle, p.value, src.ctypes.data, n), "h2d")
+        coll = bdist.TorchCollective(ctx, None, 2)
+        t = coll._device(p.value, n)
+        assert t.is_cuda and t.dtype == torch.uint8 and t.numel() == n
+        assert t.data_ptr() == p.value
+        assert np.array_equal(t.cpu().numpy(), src)
+        t.fill_(7)
+        torch.cuda.synchronize()
+        back = np.empty(n, dtype=np.uint8)
+        bnpp._check(bnpp._lib.bnpp_memcpy_d2h(ctx.handle, back.ctypes.data, p.value, n), "d2h")
+        assert (back == 7).all()
+    finally:
+        bnpp._lib.bnpp_free(ctx.handle, p)
