@@ -157,11 +157,42 @@ def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_or
         rec["check"] = {"method": "P(x_t=0) vs Z(x_t=0)/Z from conditioned partitions", "abs_err": errs,
                         "max_abs_err": max(errs.values()), "tolerance": tol,
                         "ok": max(errs.values()) <= tol}
+    if world > 1 and world & (world - 1) == 0 and column_order and os.environ.get("BNPP_BENCH_SLICED", "1") != "0":
+        rec["sliced"] = sliced_mar(ctx, rank, world, dist, dev, m, order, dt, marg)
     # the reference cannot run it (min-fill width 46 at 32x32); lower bound
     # (filled in by reference_bound once the CPU rate is measured): one VE
     # per variable, each at least the column-sweep PR's factor-entries
     rec["_bound"] = (m.n_vars, bnpp.plan_stats(m, 0, {}, "mf", dtype=dt, order=order)[0], rows)
     return rec
+
+
+def sliced_mar(ctx, rank, world, dist, dev, m, order, dt, marg_ref):
+    """The same marginals with every message sliced over the ranks
+    (bnpp.dist.sliced_tree_marginals): wall-clock max over ranks,
+    cold and warm, and the largest difference from the segment scheme's
+    marginals.  Guarded: its collectives run in process groups with a 120-s
+    timeout, and any failure is recorded instead of ending the bench."""
+    import torch
+    from bnpp import dist as bdist
+
+    def timed():
+        dist.barrier()
+        t0 = time.perf_counter()
+        mg, st = bdist.sliced_tree_marginals(ctx, m, rank, world, dist, {}, "mf", dt, order, timeout_s=120)
+        ms = (time.perf_counter() - t0) * 1e3
+        tt = torch.tensor([ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return mg, st, tt.item()
+
+    try:
+        _, _, cold = timed()
+        mg, st, warm = timed()
+        diff = max(max(abs(a - b) for a, b in zip(mg[t], marg_ref[t])) for t in marg_ref)
+        return {"wall_ms": warm, "cold_wall_ms": cold, "exchanges_per_call": st["calls"],
+                "bytes_sent_per_rank": st["bytes_sent"], "max_abs_diff_vs_segment_scheme": diff,
+                "ok": diff <= (2e-6 if dt == 1 else 1e-11)}
+    except Exception as e:                                  # recorded, not fatal
+        return {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
 
 
 def secondary_mar(ctx, name: str, with_reference: bool):

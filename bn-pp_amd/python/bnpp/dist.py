@@ -130,12 +130,18 @@ class TorchCollective:
     the next kernel after RCCL.  gloo (tests, CPU): the engine's stream is
     synchronised, the bytes staged through host memory."""
 
-    def __init__(self, ctx, dist, world: int):
+    def __init__(self, ctx, dist, world: int, timeout_s: float = 0):
         import bnpp
         self.ctx, self.dist, self.world, self.bnpp = ctx, dist, world, bnpp
-        self.backend = dist.get_backend() if dist.is_initialized() else "gloo"
+        self.backend = dist.get_backend() if dist is not None and dist.is_initialized() else "gloo"
         self.calls = 0
         self.bytes_sent = 0
+        # nccl: one process group per engine stream (the two lanes of a
+        # two-front schedule exchange concurrently, each on its own
+        # communicator); created at a lane's first exchange, which every rank
+        # reaches in the same order
+        self.groups = {}
+        self.timeout_s = timeout_s
 
     def _host(self, ptr: int, nbytes: int):
         import numpy as np
@@ -161,14 +167,22 @@ class TorchCollective:
         R = self.world
         self.bytes_sent += nbytes * (R - 1)
         if self.backend == "nccl":
+            if stream not in self.groups:
+                if self.timeout_s > 0:
+                    import datetime
+                    self.groups[stream] = self.dist.new_group(backend="nccl",
+                                                              timeout=datetime.timedelta(seconds=self.timeout_s))
+                else:
+                    self.groups[stream] = self.dist.new_group(backend="nccl")
+            grp = self.groups[stream]
             s = torch.cuda.ExternalStream(stream)
             with torch.cuda.stream(s):
                 st = self._device(send, nbytes * (R if op == bnpp.COLL_ALLTOALL else 1))
                 rt = self._device(recv, nbytes * R)
                 if op == bnpp.COLL_ALLGATHER:
-                    self.dist.all_gather_into_tensor(rt, st)
+                    self.dist.all_gather_into_tensor(rt, st, group=grp)
                 else:
-                    self.dist.all_to_all_single(rt, st)
+                    self.dist.all_to_all_single(rt, st, group=grp)
             return
         bnpp._check(bnpp._lib.bnpp_synchronize(self.ctx.handle, stream), "bnpp_synchronize")
         st = self._host(send, nbytes * (R if op == bnpp.COLL_ALLTOALL else 1))
@@ -235,12 +249,12 @@ def torch_min_budget_gb(dist) -> float:
 
 
 def sliced_tree_marginals(ctx, model, rank: int, world: int, dist=None, evidence=None, heuristic: str = "mf",
-                          dtype=None, order=None):
+                          dtype=None, order=None, timeout_s: float = 0):
     """Bucket-tree marginals with every message sliced over `world` ranks
     (bnpp_marginals_tree_sliced): -> ({var: marginal}, collective stats)."""
     import bnpp
 
-    coll = TorchCollective(ctx, dist, world)
+    coll = TorchCollective(ctx, dist, world, timeout_s)
     # every rank must plan the same checkpoint count (the exchanges are
     # collectives): the smallest free memory of the world sets the budget
     budget = torch_min_budget_gb(dist)
