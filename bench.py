@@ -157,7 +157,11 @@ def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_or
         rec["check"] = {"method": "P(x_t=0) vs Z(x_t=0)/Z from conditioned partitions", "abs_err": errs,
                         "max_abs_err": max(errs.values()), "tolerance": tol,
                         "ok": max(errs.values()) <= tol}
-    if world > 1 and world & (world - 1) == 0 and column_order and os.environ.get("BNPP_BENCH_SLICED", "1") != "0":
+    # sliced messages pay off from 4 ranks (2 ranks: one xGMI link carries 7/8
+    # of every re-sliced message); BNPP_BENCH_SLICED=0 skips it
+    sliced_min = 2 if os.environ.get("BNPP_BENCH_REHEARSE") == "1" else 4
+    if world >= sliced_min and world & (world - 1) == 0 and column_order and \
+            os.environ.get("BNPP_BENCH_SLICED", "1") != "0":
         rec["sliced"] = sliced_mar(ctx, rank, world, dist, dev, m, order, dt, marg)
     # the reference cannot run it (min-fill width 46 at 32x32); lower bound
     # (filled in by reference_bound once the CPU rate is measured): one VE

@@ -706,6 +706,17 @@ int bnpp_ctx_destroy(bnpp_ctx *ctx) {
     return BNPP_OK;
 }
 
+int bnpp_ctx_trim(bnpp_ctx *ctx) {
+    if (!ctx) return set_err(BNPP_ERR_INVALID, "null context");
+    std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
+    if (!lk.owns_lock()) return set_err(BNPP_ERR_INVALID, "a call on this context is running");
+    (void)hipSetDevice(ctx->c.device);
+    (void)hipDeviceSynchronize();
+    drop_arena_cache(ctx->c);
+    drop_buffer_cache(ctx->c);
+    return BNPP_OK;
+}
+
 int bnpp_ctx_stream(bnpp_ctx *ctx, void **stream) {
     if (!ctx || !stream) return set_err(BNPP_ERR_INVALID, "null argument");
     *stream = ctx->c.stream;

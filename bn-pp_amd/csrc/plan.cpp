@@ -1621,6 +1621,12 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             pi_pos = std::min(pi_pos, j);
         };
         int next_deliver = (int)D.size() - 1;
+        if (std::getenv("BNPP_DEBUG_CHAIN_PLAN")) {
+            std::fprintf(stderr, "[chain plan] path of %d buckets, segment [%d, %d), %zu deliveries, %d slots, lanes %d:", m, a,
+                         b, D.size(), slots, (int)lanes);
+            for (int d : D) std::fprintf(stderr, " %d", d);
+            std::fprintf(stderr, "\n");
+        }
         // the marginals delivered at position j from its belief (lam_j, pi_j)
         auto deliver_bel = [&](int j, const std::vector<View> &bel) {
             const std::vector<int> &Sj = Sof(win[j]);          // conditioned away on this rank
@@ -1708,19 +1714,68 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         };
         // reverse(lo, hi, start, spos, s): deliver D[hi-1] ... D[lo] (binomial
         // checkpointing over the deliveries); `start` = lam at spos < D[lo]
+        // Where to checkpoint: the split of [lo, hi) with sl slots that
+        // minimises the forward work, each step weighted by its message's
+        // entries (a chain's first deliveries are one bucket apart over tiny
+        // messages, the rest ~24 buckets apart over 2^32-entry ones: the
+        // uniform-step binomial rule spent the slots on the cheap ones and
+        // recomputed the expensive tail; 32x32: 213 -> ~140 forward runs).
+        // cost(lo, hi, s), start = D[lo-1] (the prefix end for lo = 0):
+        //   s = 0: sum_i adv(start, D[i]);  else min_c adv(start, D[c]) +
+        //   cost(c+1, hi, s-1) + cost(lo, c, s).  O(n^3 s / 6); long delivery
+        // lists (> 256) keep the binomial rule.
+        const int nD = (int)D.size();
+        const int sp0 = nD ? D[0] - 1 : -1;
+        std::vector<double> Wc(m + 1, 0.0);                    // Wc[i + 1] = entries of lam_0..lam_i
+        for (int i = 0; i < m; ++i) Wc[i + 1] = Wc[i] + (double)table_size(lam_vars[path[i]], cards);
+        auto adv_cost = [&](int from, int to) { return Wc[to + 1] - Wc[from + 1]; };
+        const bool use_dp = !lanes && nD > 0 && nD <= 256 && !std::getenv("BNPP_BINOMIAL_REVOLVE");
+        const int S = use_dp ? std::min(slots, nD) : 0;
+        std::vector<double> cost;
+        std::vector<int16_t> arg;
+        auto at = [&](int lo, int hi, int sl) { return ((size_t)lo * (nD + 1) + hi) * (S + 1) + sl; };
+        if (use_dp) {
+            cost.assign((size_t)(nD + 1) * (nD + 1) * (S + 1), 0.0);
+            arg.assign(cost.size(), -1);
+            for (int len = 1; len <= nD; ++len)
+                for (int lo = 0; lo + len <= nD; ++lo) {
+                    const int hi = lo + len, st = lo ? D[lo - 1] : sp0;
+                    double c0 = 0;
+                    for (int i = lo; i < hi; ++i) c0 += adv_cost(st, D[i]);
+                    cost[at(lo, hi, 0)] = c0;
+                    for (int sl = 1; sl <= S; ++sl) {
+                        double best = c0;
+                        int bc = -1;
+                        for (int c = lo; c < hi; ++c) {
+                            const double v = adv_cost(st, D[c]) + cost[at(c + 1, hi, sl - 1)] + cost[at(lo, c, sl)];
+                            if (v < best) {
+                                best = v;
+                                bc = c;
+                            }
+                        }
+                        cost[at(lo, hi, sl)] = best;
+                        arg[at(lo, hi, sl)] = (int16_t)bc;
+                    }
+                }
+        }
         std::function<void(int, int, const View *, int, int)> reverse = [&](int rlo, int rhi, const View *start,
                                                                              int spos, int sl) {
             const int len = rhi - rlo;
             if (len <= 0 || !ok) return;
-            if (len == 1 || sl <= 0) {
+            int c = -1;
+            if (use_dp) {
+                c = arg[at(rlo, rhi, std::min(sl, S))];
+            } else if (len > 1 && sl > 0) {
+                int r = 1;
+                while (binom_capped(sl + r, sl) < len) ++r;
+                int64_t right_cap = binom_capped(sl - 1 + r, sl - 1);
+                int d = (int)std::max<int64_t>(1, len - std::min<int64_t>(right_cap, len - 1));
+                c = rlo + d - 1;
+            }
+            if (c < 0) {                                       // no checkpoint: every delivery from `start`
                 for (int i = rhi - 1; i >= rlo; --i) ok = ok && deliver(i, advance(start, spos, D[i]));
                 return;
             }
-            int r = 1;
-            while (binom_capped(sl + r, sl) < len) ++r;
-            int64_t right_cap = binom_capped(sl - 1 + r, sl - 1);
-            int d = (int)std::max<int64_t>(1, len - std::min<int64_t>(right_cap, len - 1));
-            const int c = rlo + d - 1;
             View ck = advance(start, spos, D[c]);
             reverse(c + 1, rhi, &ck, D[c], sl - 1);
             ok = ok && deliver(c, ck);

@@ -50,6 +50,7 @@ _SIGS = {
     "bnpp_ctx_create": (_I, [_I, C.POINTER(_P)]),
     "bnpp_ctx_destroy": (_I, [_P]),
     "bnpp_ctx_stream": (_I, [_P, C.POINTER(_P)]),
+    "bnpp_ctx_trim": (_I, [_P]),
     "bnpp_malloc": (_I, [_P, C.c_size_t, C.POINTER(_P)]),
     "bnpp_free": (_I, [_P, _P]),
     "bnpp_memcpy_h2d": (_I, [_P, _P, _P, C.c_size_t]),
@@ -151,6 +152,10 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def trim(self) -> None:
+        """Release the device memory kept between calls (cached arena, buffers)."""
+        _check(_lib.bnpp_ctx_trim(self.handle), "bnpp_ctx_trim")
 
     def stream(self) -> int:
         s = _P()

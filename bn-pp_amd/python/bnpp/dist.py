@@ -255,6 +255,12 @@ def sliced_tree_marginals(ctx, model, rank: int, world: int, dist=None, evidence
     import bnpp
 
     coll = TorchCollective(ctx, dist, world, timeout_s)
+    if not getattr(ctx, "_sliced_trimmed", False):
+        # the first sliced call on this context: what it cached for other
+        # calls (e.g. a segment-scheme arena) is freed, so the budget below
+        # sees it; later calls reuse the sliced job's own cached arena
+        ctx.trim()
+        ctx._sliced_trimmed = True
     # every rank must plan the same checkpoint count (the exchanges are
     # collectives): the smallest free memory of the world sets the budget
     budget = torch_min_budget_gb(dist)

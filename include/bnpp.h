@@ -78,6 +78,9 @@ int bnpp_device_count(int *n);
 int bnpp_ctx_create(int device, bnpp_ctx **out);
 int bnpp_ctx_destroy(bnpp_ctx *ctx);
 int bnpp_ctx_stream(bnpp_ctx *ctx, void **stream);
+/* release the device memory the context keeps between calls (the cached arena
+ * of the last partition / marginals call and the small-buffer cache) */
+int bnpp_ctx_trim(bnpp_ctx *ctx);
 int bnpp_malloc(bnpp_ctx *ctx, size_t bytes, void **dptr);
 int bnpp_free(bnpp_ctx *ctx, void *dptr);
 int bnpp_memcpy_h2d(bnpp_ctx *ctx, void *dst, const void *src, size_t bytes);
