@@ -184,6 +184,9 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
 #ifndef BNPP_SPLIT_FLAT
 #define BNPP_SPLIT_FLAT 0     // 1: one tile per workgroup (flat grid), no prefetch
 #endif
+#ifndef BNPP_SPLIT_FWD_MODE
+#define BNPP_SPLIT_FWD_MODE 0 // single-run forward loop: 0 two register sets alternating, 1 rotation, 2 one tile ahead
+#endif
 #ifndef BNPP_SPLIT_NTL
 #define BNPP_SPLIT_NTL 0      // nontemporal message loads
 #endif
@@ -502,7 +505,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     float rg[16];
     int64_t in_off, out_off;
     int32_t gb[F];
-    if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0 && FORM == kChainBwd) {
+    if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0 && (FORM == kChainBwd || BNPP_SPLIT_FWD_MODE == 2)) {
         // one bucket, backward form: the next tile's loads are issued
         // (unconditionally: the last tile is re-read rather than branching, so
         // the wait counts stay static) before the current tile is computed (a
@@ -519,6 +522,28 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             decode(vb, in_off, out_off, gb);
             run_tile(t, out_off, gb);
             vb = vbn;
+            if (vb >= total_vblocks) break;
+        }
+    } else if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0 && BNPP_SPLIT_FWD_MODE == 1) {
+        // forward, two tiles in flight by rotation (t <- A <- B <- new loads)
+        const int64_t last = total_vblocks - 1, g = gridDim.x;
+        auto clamp = [&](int64_t v) { return v < last ? v : last; };
+        float rb[16];
+        decode(vb, in_off, out_off, gb);
+        issue(in_off, rg);
+        decode(clamp(vb + g), in_off, out_off, gb);
+        issue(in_off, rb);
+        while (true) {
+            float t[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) t[e] = rg[e];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) rg[e] = rb[e];
+            decode(clamp(vb + 2 * g), in_off, out_off, gb);
+            issue(in_off, rb);
+            decode(vb, in_off, out_off, gb);
+            run_tile(t, out_off, gb);
+            vb += g;
             if (vb >= total_vblocks) break;
         }
     } else if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0) {
