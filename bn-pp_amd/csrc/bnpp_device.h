@@ -196,4 +196,46 @@ struct BpArgs {
     int32_t *iterations;
 };
 
+// Multi-workgroup flood (bp.hip, bp_flood_*): the same schedule as BpArgs's
+// one-workgroup loop, one launch per phase and iteration, for models whose
+// per-iteration work would keep one workgroup busy for long (or whose tables
+// pass 2^31 entries).  A factor->variable message entry t is a sum over
+// n_f / r terms; it is cut into segments of at most kBpSegTerms terms, held
+// in entry order (segments of entry t: [seg_off[t], seg_off[t+1]), term
+// ranges ascending), each summed by a group of G lanes into part[segment]; the
+// finishing launch adds an entry's parts in order.  err is a ring of
+// kBpErrRing per-iteration maxima (fp64 bit patterns: non-negative doubles
+// order like their bits); a launch of iteration it returns at once when
+// iteration it-1 already met the tolerance.
+constexpr int kBpFloodBlock = 256;
+constexpr uint64_t kBpSegTerms = 16384;     // 64 lanes x 256 terms
+constexpr int kBpErrChunk = 32;             // iterations per host check
+constexpr int kBpErrRing = 2 * kBpErrChunk;
+struct BpFlood {
+    int32_t n_vars, n_edges, n_msg;
+    int32_t idx64;                          // 64-bit table indices for every factor (test knob)
+    int32_t one_seg;                        // every entry is one segment (segment t = entry t)
+    double eps;
+    const int32_t *cards;
+    const double *tables;
+    const int64_t *tab_off;                 // n_factors + 1 (entries)
+    const int32_t *f_edge_off;              // n_factors + 1
+    const int32_t *edge_var, *edge_fac;     // n_edges
+    const uint64_t *edge_stride;            // n_edges
+    const int32_t *msg_off;                 // n_edges + 1
+    const int32_t *item_edge;               // n_msg
+    const int64_t *seg_off;                 // n_msg + 1
+    const int32_t *seg_item;                // per segment: its message entry
+    const uint64_t *seg_q0;                 // per segment: first term
+    // segments by lane class c: cls_seg[cls_pos[c] .. cls_pos[c+1]), blocks
+    // [cls_blk[c], cls_blk[c+1]) of the factor->variable launch
+    int64_t cls_pos[5];
+    int32_t cls_blk[5];
+    const int32_t *cls_seg;
+    const int32_t *v_edge_off, *v_moff;     // n_vars + 1; per edge of a variable: msg_off of that edge
+    const int32_t *marg_off;                // n_vars + 1
+    double *v2f, *f2v, *raw, *part, *marg;
+    unsigned long long *err;                // kBpErrRing
+};
+
 }  // namespace bnpp

@@ -26,7 +26,7 @@
 
 using namespace bnpp;
 
-constexpr int kTimingPhases = 8;
+constexpr int kTimingPhases = 9;
 
 struct bnpp_ctx {
     Context c;
@@ -521,7 +521,8 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     g_timing[0] = t0 - tp;
     g_timing[1] = t1 - t0;
     g_timing[2] = now_ms() - t1;
-    g_timing[7] = job->pg.arena_cached && use_cache ? 1.0 : 0.0;
+    g_timing[7] = job->pg.arena_reused ? 1.0 : 0.0;
+    g_timing[8] = job->pg.arena_alloc_ms;
     if (std::getenv("BNPP_TIMING"))
         std::fprintf(stderr, "[bnpp] job: upload %.1f ms, program (arena %.2f GB) %.1f ms\n", t1 - t0,
                      job->pg.arena_bytes / 1e9, now_ms() - t1);
@@ -1272,11 +1273,231 @@ int bnpp_plan_tree_sliced(const bnpp_model *m, int n_ev, const int *ev_vars, con
     BNPP_GUARD_END
 }
 
+// Loopy BP as one launch per phase and iteration (bp.hip bp_flood_*, the
+// layout of BpFlood): the choice for models whose iteration is too much work
+// for one workgroup and for tables of 2^31 entries or more.  The host checks
+// the per-iteration maxima every kBpErrChunk iterations; launches after the
+// converging iteration return at once on the device.
+// one-workgroup loop up to this much work per iteration (f2v terms x scope
+// size + v2f products), the flood beyond (tools/bp_modes.py: a 12x12 Ising
+// grid, work 1.2e4, 11 us per iteration in one workgroup against 24 us
+// flooded; 32x32, 8.3e4: 61 against 22 us)
+constexpr double kBpMultiWork = 32768.0;
+
+static int sum_product_flood(bnpp_ctx *ctx, const ModelData &d, int max_iter, double eps, double *out,
+                             int *iterations, double *uptime_ms, double t0) {
+    const int nv = (int)d.cards.size(), nf = (int)d.scopes.size();
+    std::vector<int32_t> f_edge_off(nf + 1, 0), edge_var, edge_fac, msg_off(1, 0), item_edge, v_edge_off(nv + 1, 0),
+        v_edges, marg_off(nv + 1, 0);
+    std::vector<uint64_t> edge_stride;
+    std::vector<int64_t> tab_off(nf + 1, 0);
+    for (int f = 0; f < nf; ++f) {
+        const std::vector<int> &sc = d.scopes[f];
+        uint64_t size = 1;
+        for (int v : sc) size *= (uint64_t)d.cards[v];
+        uint64_t st = size;
+        for (size_t j = 0; j < sc.size(); ++j) {
+            st /= (uint64_t)d.cards[sc[j]];
+            const int e = (int)edge_var.size();
+            edge_var.push_back(sc[j]);
+            edge_fac.push_back(f);
+            edge_stride.push_back(st);
+            for (int x = 0; x < d.cards[sc[j]]; ++x) item_edge.push_back(e);
+            if ((int64_t)msg_off.back() + d.cards[sc[j]] >= INT32_MAX)
+                return set_err(BNPP_ERR_UNSUPPORTED, "sum-product: more than 2^31 message entries");
+            msg_off.push_back(msg_off.back() + d.cards[sc[j]]);
+            ++v_edge_off[sc[j] + 1];
+        }
+        f_edge_off[f + 1] = (int32_t)edge_var.size();
+        tab_off[f + 1] = tab_off[f] + (int64_t)size;
+    }
+    const int ne = (int)edge_var.size(), nmsg = msg_off.back();
+    for (int v = 0; v < nv; ++v) {
+        v_edge_off[v + 1] += v_edge_off[v];
+        marg_off[v + 1] = marg_off[v] + d.cards[v];
+    }
+    v_edges.resize(ne);
+    {
+        std::vector<int32_t> fill(v_edge_off.begin(), v_edge_off.end() - 1);
+        for (int e = 0; e < ne; ++e) v_edges[fill[edge_var[e]]++] = msg_off[e];   // ascending edge = factor id
+    }
+    // segments in entry order, then their lane classes
+    std::vector<int64_t> seg_off(nmsg + 1, 0);
+    for (int t = 0; t < nmsg; ++t) {
+        const int e = item_edge[t];
+        const uint64_t terms = (uint64_t)(tab_off[edge_fac[e] + 1] - tab_off[edge_fac[e]]) / d.cards[edge_var[e]];
+        seg_off[t + 1] = seg_off[t] + (int64_t)std::max<uint64_t>(1, (terms + kBpSegTerms - 1) / kBpSegTerms);
+    }
+    const int64_t nseg = seg_off[nmsg];
+    if (nseg >= INT32_MAX) return set_err(BNPP_ERR_UNSUPPORTED, "sum-product: more than 2^31 segments");
+    std::vector<int32_t> seg_item(nseg), cls[4];
+    std::vector<uint64_t> seg_q0(nseg);
+    for (int t = 0; t < nmsg; ++t) {
+        const int e = item_edge[t];
+        const uint64_t terms = (uint64_t)(tab_off[edge_fac[e] + 1] - tab_off[edge_fac[e]]) / d.cards[edge_var[e]];
+        for (int64_t s = seg_off[t]; s < seg_off[t + 1]; ++s) {
+            const uint64_t q0 = (uint64_t)(s - seg_off[t]) * kBpSegTerms;
+            seg_item[s] = t;
+            seg_q0[s] = q0;
+            cls[bp_lane_class((int64_t)std::min<uint64_t>(kBpSegTerms, terms - std::min(q0, terms)))].push_back((int32_t)s);
+        }
+    }
+    std::vector<int32_t> cls_seg;
+    cls_seg.reserve(nseg);
+    BpFlood a{};
+    const int lanes[4] = {1, 4, 16, 64};
+    for (int c = 0; c < 4; ++c) {
+        a.cls_pos[c] = (int64_t)cls_seg.size();
+        cls_seg.insert(cls_seg.end(), cls[c].begin(), cls[c].end());
+        a.cls_pos[c + 1] = (int64_t)cls_seg.size();
+        const int64_t per_block = kBpFloodBlock / lanes[c];
+        const int64_t blocks = ((int64_t)cls[c].size() + per_block - 1) / per_block;
+        if ((int64_t)a.cls_blk[c] + blocks >= INT32_MAX) return set_err(BNPP_ERR_UNSUPPORTED, "sum-product: grid too large");
+        a.cls_blk[c + 1] = a.cls_blk[c] + (int32_t)blocks;
+    }
+    // device block: index arrays (256-B aligned pieces), tables, messages
+    size_t off = 0;
+    auto place = [&](size_t bytes) {
+        const size_t o = off;
+        off = (off + bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    const size_t o_cards = place(4 * (size_t)nv), o_tab_off = place(8 * (size_t)(nf + 1)),
+                 o_feo = place(4 * (size_t)(nf + 1)), o_ev = place(4 * (size_t)ne), o_ef = place(4 * (size_t)ne),
+                 o_es = place(8 * (size_t)ne), o_mo = place(4 * (size_t)(ne + 1)), o_ie = place(4 * (size_t)nmsg),
+                 o_so = place(8 * (size_t)(nmsg + 1)), o_si = place(4 * (size_t)nseg), o_sq = place(8 * (size_t)nseg),
+                 o_cs = place(4 * (size_t)nseg), o_veo = place(4 * (size_t)(nv + 1)), o_ve = place(4 * (size_t)ne),
+                 o_mgo = place(4 * (size_t)(nv + 1));
+    const size_t idx_bytes = off;
+    const size_t o_tabs = place(8 * (size_t)tab_off[nf]);
+    const size_t o_v2f = place(8 * (size_t)nmsg), o_f2v = place(8 * (size_t)nmsg), o_raw = place(8 * (size_t)nmsg),
+                 o_part = place(8 * (size_t)nseg), o_marg = place(8 * (size_t)marg_off[nv]),
+                 o_err = place(8 * (size_t)kBpErrRing);
+    std::vector<unsigned char> host(idx_bytes);
+    auto put = [&](size_t o, const void *src, size_t bytes) {
+        if (bytes) std::memcpy(host.data() + o, src, bytes);
+    };
+    std::vector<int32_t> cards32(d.cards.begin(), d.cards.end());
+    put(o_cards, cards32.data(), 4 * (size_t)nv);
+    put(o_tab_off, tab_off.data(), 8 * tab_off.size());
+    put(o_feo, f_edge_off.data(), 4 * f_edge_off.size());
+    put(o_ev, edge_var.data(), 4 * (size_t)ne);
+    put(o_ef, edge_fac.data(), 4 * (size_t)ne);
+    put(o_es, edge_stride.data(), 8 * (size_t)ne);
+    put(o_mo, msg_off.data(), 4 * msg_off.size());
+    put(o_ie, item_edge.data(), 4 * (size_t)nmsg);
+    put(o_so, seg_off.data(), 8 * seg_off.size());
+    put(o_si, seg_item.data(), 4 * (size_t)nseg);
+    put(o_sq, seg_q0.data(), 8 * (size_t)nseg);
+    put(o_cs, cls_seg.data(), 4 * (size_t)nseg);
+    put(o_veo, v_edge_off.data(), 4 * v_edge_off.size());
+    put(o_ve, v_edges.data(), 4 * (size_t)ne);
+    put(o_mgo, marg_off.data(), 4 * marg_off.size());
+
+    hipStream_t s = ctx->c.stream;
+    unsigned char *dev = nullptr;
+    if (hipSetDevice(ctx->c.device) != hipSuccess) return set_err(BNPP_ERR_HIP, "sum-product: hipSetDevice");
+    if (hipMalloc(&dev, off) != hipSuccess) return set_err(BNPP_ERR_OOM, "sum-product: device allocation");
+    struct Free {
+        unsigned char *p;
+        ~Free() { (void)hipFree(p); }
+    } guard{dev};
+    a.n_vars = nv;
+    a.n_edges = ne;
+    a.n_msg = nmsg;
+    a.idx64 = std::getenv("BNPP_BP_IDX64") ? 1 : 0;
+    a.one_seg = nseg == nmsg ? 1 : 0;
+    a.eps = eps;
+    a.cards = reinterpret_cast<const int32_t *>(dev + o_cards);
+    a.tables = reinterpret_cast<const double *>(dev + o_tabs);
+    a.tab_off = reinterpret_cast<const int64_t *>(dev + o_tab_off);
+    a.f_edge_off = reinterpret_cast<const int32_t *>(dev + o_feo);
+    a.edge_var = reinterpret_cast<const int32_t *>(dev + o_ev);
+    a.edge_fac = reinterpret_cast<const int32_t *>(dev + o_ef);
+    a.edge_stride = reinterpret_cast<const uint64_t *>(dev + o_es);
+    a.msg_off = reinterpret_cast<const int32_t *>(dev + o_mo);
+    a.item_edge = reinterpret_cast<const int32_t *>(dev + o_ie);
+    a.seg_off = reinterpret_cast<const int64_t *>(dev + o_so);
+    a.seg_item = reinterpret_cast<const int32_t *>(dev + o_si);
+    a.seg_q0 = reinterpret_cast<const uint64_t *>(dev + o_sq);
+    a.cls_seg = reinterpret_cast<const int32_t *>(dev + o_cs);
+    a.v_edge_off = reinterpret_cast<const int32_t *>(dev + o_veo);
+    a.v_moff = reinterpret_cast<const int32_t *>(dev + o_ve);
+    a.marg_off = reinterpret_cast<const int32_t *>(dev + o_mgo);
+    a.v2f = reinterpret_cast<double *>(dev + o_v2f);
+    a.f2v = reinterpret_cast<double *>(dev + o_f2v);
+    a.raw = reinterpret_cast<double *>(dev + o_raw);
+    a.part = reinterpret_cast<double *>(dev + o_part);
+    a.marg = reinterpret_cast<double *>(dev + o_marg);
+    a.err = reinterpret_cast<unsigned long long *>(dev + o_err);
+    hipError_t e = hipMemcpyAsync(dev, host.data(), idx_bytes, hipMemcpyHostToDevice, s);
+    // tables: small ones gathered into a bounded staging buffer (one copy per
+    // 256 MB: a grid has ~10^5 factors, and a copy per factor costs ~3 us of
+    // host time), tables of 64 MB and more copied straight from the model
+    {
+        constexpr size_t kStage = (size_t)256 << 20, kDirect = (size_t)64 << 20;
+        std::vector<unsigned char> stage;
+        size_t at = o_tabs;                                   // device offset of stage[0]
+        auto flush = [&]() {
+            if (!stage.empty() && e == hipSuccess) {
+                e = hipMemcpyAsync(dev + at, stage.data(), stage.size(), hipMemcpyHostToDevice, s);
+                if (e == hipSuccess) e = hipStreamSynchronize(s);      // stage is reused
+            }
+            at += stage.size();
+            stage.clear();
+        };
+        for (int f = 0; f < nf && e == hipSuccess; ++f) {
+            const size_t bytes = 8 * d.values[f].size();
+            if (bytes >= kDirect) {
+                flush();
+                e = hipMemcpyAsync(dev + at, d.values[f].data(), bytes, hipMemcpyHostToDevice, s);
+                at += bytes;
+                continue;
+            }
+            if (stage.size() + bytes > kStage) flush();
+            const unsigned char *p = reinterpret_cast<const unsigned char *>(d.values[f].data());
+            stage.insert(stage.end(), p, p + bytes);
+        }
+        flush();
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(a.err, 0, 8 * (size_t)kBpErrRing, s);
+    if (e == hipSuccess) e = launch_bp_flood_init(a, s);
+    int it_done = max_iter;
+    std::vector<unsigned long long> chunk(kBpErrChunk);
+    for (int c = 0; e == hipSuccess && (int64_t)c * kBpErrChunk < max_iter; ++c) {
+        const int it0 = c * kBpErrChunk, it1 = std::min(max_iter, it0 + kBpErrChunk);
+        unsigned long long *half = a.err + (c % 2) * kBpErrChunk;
+        e = hipMemsetAsync(half, 0, 8 * (size_t)kBpErrChunk, s);
+        for (int it = it0; it < it1 && e == hipSuccess; ++it) e = launch_bp_flood_iteration(a, it, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(chunk.data(), half, 8 * (size_t)(it1 - it0), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        bool done = false;
+        for (int it = it0; e == hipSuccess && it < it1; ++it) {
+            double m;
+            std::memcpy(&m, &chunk[it - it0], 8);
+            if (m < eps) {                        // graph.cpp:328
+                it_done = it;
+                done = true;
+                break;
+            }
+        }
+        if (done) break;
+    }
+    if (e == hipSuccess) e = launch_bp_flood_marginals(a, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, a.marg, 8 * (size_t)marg_off[nv], hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return set_err(BNPP_ERR_HIP, std::string("sum-product: ") + hipGetErrorString(e));
+    if (iterations) *iterations = it_done;
+    if (uptime_ms) *uptime_ms = now_ms() - t0;
+    return BNPP_OK;
+}
+
 // BN::marginals with options["sum-product"] (model.cpp:313-317): loopy BP on
 // the factor graph of the model's own factors (evidence is not used on this
 // path, as in the reference), FactorGraph::update(max_iter, eps) then one
 // marginal per variable (graph.cpp:256-403).  One workgroup runs the whole
-// loop (bp.hip).
+// loop (bp.hip) unless the iteration's work calls for the multi-workgroup
+// flood above.
 int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double eps, double *out, int *iterations,
                      double *uptime_ms) {
     BNPP_GUARD_BEGIN
@@ -1285,6 +1506,32 @@ int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double ep
     const double t0 = now_ms();
     const ModelData &d = m->d;
     const int nv = (int)d.cards.size(), nf = (int)d.scopes.size();
+    // one workgroup for the whole loop, or one launch per phase and iteration
+    // (BNPP_BP_MODE=single|multi overrides the choice by work per iteration)
+    bool big_table = false;
+    double work = 0.0;
+    {
+        std::vector<double> deg(nv, 0.0);
+        for (int f = 0; f < nf; ++f) {
+            double size = 1.0;
+            for (int v : d.scopes[f]) {
+                size *= d.cards[v];
+                deg[v] += 1.0;
+            }
+            const double m = (double)d.scopes[f].size();
+            work += size * m * m;
+            big_table |= size >= 2147483648.0;
+        }
+        for (int v = 0; v < nv; ++v) work += deg[v] * deg[v] * d.cards[v];
+    }
+    const char *mode = std::getenv("BNPP_BP_MODE");
+    bool multi = big_table || work > kBpMultiWork;
+    if (mode && !std::strcmp(mode, "multi")) multi = true;
+    if (mode && !std::strcmp(mode, "single")) {
+        if (big_table) return set_err(BNPP_ERR_UNSUPPORTED, "sum-product: one-workgroup loop needs tables < 2^31 entries");
+        multi = false;
+    }
+    if (multi) return sum_product_flood(ctx, d, max_iter, eps, out, iterations, uptime_ms, t0);
     // host image of every input array, laid out as on the device
     std::vector<int32_t> f_edge_off(nf + 1, 0), edge_var, edge_fac, msg_off(1, 0), item_edge, v_edge_off(nv + 1, 0),
         v_edges, marg_off(nv + 1, 0);
@@ -1294,7 +1541,6 @@ int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double ep
         const std::vector<int> &sc = d.scopes[f];
         int64_t size = 1;
         for (int v : sc) size *= d.cards[v];
-        if (size >= ((int64_t)1 << 31)) return set_err(BNPP_ERR_UNSUPPORTED, "sum-product: factor table >= 2^31 entries");
         int64_t st = size;
         for (size_t j = 0; j < sc.size(); ++j) {
             st /= d.cards[sc[j]];

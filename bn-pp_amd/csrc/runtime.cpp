@@ -1,4 +1,5 @@
 // Device runtime: source upload, executable schedules, launches, result fetch.
+#include <chrono>
 #include "runtime.hpp"
 
 #include <algorithm>
@@ -344,9 +345,12 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
     if (use_cache && ctx.arena_cache && ctx.arena_cache_bytes >= need) {
         pg.arena = ctx.arena_cache;
         pg.arena_cached = true;
+        pg.arena_reused = true;
     } else {
         if (use_cache) drop_arena_cache(ctx);            // too small: replace it
+        const auto ta = std::chrono::steady_clock::now();
         if ((err = hipMalloc(&pg.arena, (size_t)need)) != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
+        pg.arena_alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
         if (use_cache) {
             ctx.arena_cache = pg.arena;
             ctx.arena_cache_bytes = need;

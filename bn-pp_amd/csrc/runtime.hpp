@@ -45,6 +45,11 @@ struct XchgHooks {
 };
 // loopy BP, one workgroup (bp.hip)
 hipError_t launch_sum_product(const BpArgs &a, hipStream_t stream);
+// multi-workgroup flood (bp.hip): messages set to 1/|x|; one iteration (three
+// launches); the marginals
+hipError_t launch_bp_flood_init(const BpFlood &a, hipStream_t stream);
+hipError_t launch_bp_flood_iteration(const BpFlood &a, int it, hipStream_t stream);
+hipError_t launch_bp_flood_marginals(const BpFlood &a, hipStream_t stream);
 
 enum DType { kF64 = 0, kF32 = 1 };
 
@@ -122,6 +127,8 @@ struct Program {
     void *arena = nullptr;
     int64_t arena_bytes = 0;
     bool arena_cached = false;          // arena is the context's cache (not freed with the program)
+    bool arena_reused = false;          // ... and was already allocated before this program
+    double arena_alloc_ms = 0;          // hipMalloc of the arena (0 when reused)
     void *results = nullptr;
     size_t results_cap = 0;
     int64_t results_bytes = 0;

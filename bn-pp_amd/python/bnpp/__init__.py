@@ -125,13 +125,13 @@ def _dbls(xs: Iterable[float]):
 
 
 TIMING_PHASES = ("plan_ms", "upload_ms", "program_ms", "launch_ms", "run_fetch_ms", "free_ms", "total_ms",
-                 "arena_reused")
+                 "arena_reused", "arena_alloc_ms")
 
 
 def last_timing() -> Dict[str, float]:
     """Phase split of this thread's last partition / marginals call (bnpp_last_timing)."""
-    out = (C.c_double * 8)()
-    _check(_lib.bnpp_last_timing(out, 8), "bnpp_last_timing")
+    out = (C.c_double * len(TIMING_PHASES))()
+    _check(_lib.bnpp_last_timing(out, len(TIMING_PHASES)), "bnpp_last_timing")
     return dict(zip(TIMING_PHASES, list(out)))
 
 
@@ -203,6 +203,22 @@ class Model:
         h = _P()
         _check(_lib.bnpp_model_from_arrays(1 if m.get("type") == "BAYES" else 0, len(m["cards"]), _ints(m["cards"]),
                                            len(widths), _ints(widths), _ints(scopes), _dbls(values), C.byref(h)),
+               "bnpp_model_from_arrays")
+        return cls(h)
+
+    @classmethod
+    def from_arrays(cls, cards: Sequence[int], scopes: Sequence[Sequence[int]], values, is_bayes: bool = False
+                    ) -> "Model":
+        """A model from one flat float64 array of every factor's table in
+        order (numpy, C-contiguous, passed by pointer: no per-entry Python
+        objects, so tables of billions of entries load in seconds)."""
+        import numpy as np
+        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1)
+        widths = [len(s) for s in scopes]
+        flat = [v for s in scopes for v in s]
+        h = _P()
+        _check(_lib.bnpp_model_from_arrays(1 if is_bayes else 0, len(cards), _ints(cards), len(widths), _ints(widths),
+                                           _ints(flat), vals.ctypes.data_as(_DP), C.byref(h)),
                "bnpp_model_from_arrays")
         return cls(h)
 
