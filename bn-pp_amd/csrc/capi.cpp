@@ -52,6 +52,10 @@ namespace {
 thread_local std::string g_err;
 // phase split of this thread's last partition / marginals call (bnpp_last_timing)
 thread_local double g_timing[kTimingPhases] = {0};
+// the context of a one-shot call being planned (create_job with the cached
+// arena): a checkpointed plan, which fills the memory budget, starts mapping
+// its arena there while the checkpoint search goes on
+thread_local Context *g_prefetch_ctx = nullptr;
 
 int set_err(int status, const std::string &msg) {
     g_err = msg;
@@ -270,6 +274,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
         } else if (need(plans.back()) > budget || n_parts > 1 || n_slices > 1) {
             // every forward message does not fit: recompute them from checkpoints
             // (chain-shaped trees), with as many checkpoint slots as fit
+            if (need(plans.back()) > budget && g_prefetch_ctx) arena_prefetch(*g_prefetch_ctx, budget);
             std::string msg;
             VEPlan best;
             // sliced runs: the two-front schedule (two concurrent lanes, no
@@ -508,6 +513,10 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     std::vector<Schedule> batches;
     if (n_parts < 1 || part < 0 || part >= n_parts) return set_err(BNPP_ERR_INVALID, "bad part / n_parts");
     const double tp = now_ms();
+    struct PrefetchScope {
+        explicit PrefetchScope(Context *c) { g_prefetch_ctx = c; }
+        ~PrefetchScope() { g_prefetch_ctx = nullptr; }
+    } prefetch_scope(use_cache ? &ctx->c : nullptr);
     int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype,
                             budget > 0 ? budget : memory_budget(ctx, use_cache), batches, job->stats, part, n_parts,
                             n_slices, slice_rank);

@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -63,6 +64,12 @@ struct Context {
     // allocator the context holds on to it until it is destroyed
     void *arena_cache = nullptr;
     int64_t arena_cache_bytes = 0;
+    // an arena being mapped on a helper thread while the host still plans
+    // (arena_prefetch): a cold call's hipMalloc of a few hundred GB costs
+    // 0.1-0.3 s, which then overlaps the checkpoint search
+    std::thread prefetch;
+    void *prefetch_ptr = nullptr;
+    int64_t prefetch_bytes = 0;
     // small device buffers (sources, descriptors, dims pool, metadata, results)
     // kept for reuse: a one-shot call otherwise pays ~10 hipMalloc / hipFree
     // pairs (hipFree synchronises), several ms of a small model's PR
@@ -152,6 +159,10 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
 hipError_t launch_copies(const CopyItem *items, int n, hipStream_t stream);
 // release the context's cached arena
 void drop_arena_cache(Context &ctx);
+// start mapping an arena of `bytes` on a helper thread unless the cached one
+// is about that big already; arena_prefetch_join makes it the cached arena
+void arena_prefetch(Context &ctx, int64_t bytes);
+void arena_prefetch_join(Context &ctx);
 int launch_program(Context &ctx, Program &pg, hipStream_t stream);
 // result values (as stored, double) and exp2 of every plan, batches in order
 int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std::vector<double>> &vals,
