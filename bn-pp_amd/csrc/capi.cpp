@@ -312,24 +312,45 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             }
             int64_t need_ok = 0, need_fail = INT64_MAX;
             bool exact = true;                            // every probe planned: the bracket is valid
-            while (lo <= hi) {
-                int mid = (lo + hi) / 2;
-                VEPlan cp;
-                if (!plan_bucket_tree_chain(d.cards, views, ord, targets, mid, part, n_parts, cp, &msg, chain_eb, n_slices,
-                                            slice_rank)) {
-                    exact = false;
-                    break;
+            // the need grows with the slot count: a k-ary search, up to 8
+            // probes planned in parallel per round (two rounds for 64 counts
+            // instead of six bisection steps; a cold call's planning time)
+            while (lo <= hi && exact) {
+                const int m = hi - lo + 1, n = std::min(8, m);
+                std::vector<int> probe(n);                // ascending, inside [lo, hi]
+                for (int i = 0; i < n; ++i) probe[i] = m <= 8 ? lo + i : lo + (int)((int64_t)m * (i + 1) / (n + 1));
+                std::vector<VEPlan> cps(n);
+                std::vector<int64_t> nb(n, 0);
+                std::vector<char> planned(n, 0);
+                std::vector<std::string> msgs(n);
+                parallel_for((int64_t)n, [&](int64_t i) {
+                    planned[i] = plan_bucket_tree_chain(d.cards, views, ord, targets, probe[i], part, n_parts, cps[i],
+                                                        &msgs[i], chain_eb, n_slices, slice_rank) ? 1 : 0;
+                    if (planned[i]) nb[i] = need(cps[i]);
+                });
+                int new_lo = lo, new_hi = hi;
+                for (int i = 0; i < n; ++i) {
+                    if (!planned[i]) {                    // as a bisection that stops at its first failure
+                        exact = false;
+                        if (msg.empty()) msg = msgs[i];
+                        new_hi = std::min(new_hi, probe[i] - 1);
+                        break;
+                    }
+                    if (nb[i] <= budget) {
+                        if (probe[i] > best_s) {
+                            best_s = probe[i];
+                            best = std::move(cps[i]);
+                        }
+                        need_ok = std::max(need_ok, nb[i]);   // valid for budgets >= every fitting probe's need
+                        new_lo = std::max(new_lo, probe[i] + 1);
+                    } else {
+                        need_fail = std::min(need_fail, nb[i]);
+                        new_hi = std::min(new_hi, probe[i] - 1);
+                        break;                            // larger probes need more still
+                    }
                 }
-                const int64_t nb = need(cp);
-                if (nb <= budget) {
-                    best_s = mid;
-                    best = std::move(cp);
-                    need_ok = std::max(need_ok, nb);      // valid for budgets >= every fitting probe's need
-                    lo = mid + 1;
-                } else {
-                    need_fail = std::min(need_fail, nb);
-                    hi = mid - 1;
-                }
+                lo = new_lo;
+                hi = new_hi;
             }
             if (best_s > 0) {
                 if (best_s != memo_s && exact) {

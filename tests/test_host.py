@@ -395,3 +395,36 @@ def test_plan_tree_sliced_shares_work_and_exchanges():
         bnpp.plan_tree_sliced(m, 0, 3, order=col)              # not a power of two
     with pytest.raises(bnpp.BnppError):
         bnpp.plan_tree_sliced(bnpp.Model.load(model_path("alarm.uai")), 0, 2)   # not a chain
+
+
+def test_checkpoint_search_picks_a_fitting_slot_count():
+    """The checkpoint-slot search (k-ary, probes planned in parallel): under
+    budgets below the full tree's arena it returns exactly the plan of one
+    fixed slot count (BNPP_TREE_SLOTS=s), the largest one whose need fits;
+    a larger budget never gives more recomputation."""
+    import os
+    from bnpp import synth
+    m = bnpp.Model.from_dict(synth.ising_grid(16, 16, seed=1))
+    col = [r * 16 + c for c in range(16) for r in range(16)]
+    full = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+    forced = {}
+    try:
+        for s in range(1, 65):
+            os.environ["BNPP_TREE_SLOTS"] = str(s)
+            forced[s] = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+    finally:
+        os.environ.pop("BNPP_TREE_SLOTS", None)
+    last = None
+    try:
+        for frac in (0.2, 0.35, 0.5, 0.7):
+            os.environ["BNPP_MEM_BUDGET_GB"] = repr(full[1] * frac / 1e9)
+            st = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+            match = [s for s, f in forced.items() if f[0] == st[0] and f[3] == st[3] and f[1] == st[1]]
+            assert match, frac
+            assert all(forced[s][1] > full[1] * frac * 0.8 for s in range(max(match) + 1, 65)
+                       if forced[s][0] < st[0]), frac         # fewer entries only by outgrowing the budget
+            if last is not None:
+                assert st[0] <= last[0]
+            last = st
+    finally:
+        os.environ.pop("BNPP_MEM_BUDGET_GB", None)
