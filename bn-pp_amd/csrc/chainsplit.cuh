@@ -190,6 +190,11 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
 #ifndef BNPP_SPLIT_NTL
 #define BNPP_SPLIT_NTL 0      // nontemporal message loads
 #endif
+// timing bisection only (results are wrong with any of these set): drop the
+// power-of-two rescale, the running maximum, the per-tile G offsets
+#ifndef BNPP_SPLIT_BISECT
+#define BNPP_SPLIT_BISECT 0   // bit 0 no rescale, bit 1 no maximum, bit 2 G offsets 0
+#endif
 #ifndef BNPP_SPLIT_WAVES
 #define BNPP_SPLIT_WAVES 0     // waves per SIMD the register allocation must allow (0: compiler's choice)
 #endif
@@ -281,7 +286,8 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             // backward) may have a G table varying along rest dim 1 (planner)
             constexpr int JR = FORM == kChainFwd ? F - 1 : 0;
 #pragma unroll
-            for (int j = 0; j < F; ++j) gb[j] = (j == JR || BNPP_DENSE_JR == 0) ? (int32_t)d1 * c.d_g1[j] : 0;
+            for (int j = 0; j < F; ++j)
+                gb[j] = (BNPP_SPLIT_BISECT & 4) == 0 && (j == JR || BNPP_DENSE_JR == 0) ? (int32_t)d1 * c.d_g1[j] : 0;
             return;
         }
         const int64_t tid0 = (vb - cur_begin) * kSplitRows;
@@ -442,12 +448,13 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             constexpr int j = 4 + decltype(jc)::value;
             split_step<F, 2, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig2);
         });
-        if (c.flags & kScale) {
+        if ((BNPP_SPLIT_BISECT & 1) == 0 && (c.flags & kScale)) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) t[e] = ldexp_t(t[e], c.neg_e);
         }
 #pragma unroll
-        for (int e = 0; e < 16; ++e) lmax = fmaxf(lmax, t[e]);      // entries are >= 0, never NaN
+        for (int e = 0; e < 16; ++e)
+            if constexpr ((BNPP_SPLIT_BISECT & 2) == 0) lmax = fmaxf(lmax, t[e]);      // entries are >= 0, never NaN
 
         if constexpr (FORM == kChainFwd) {
             // row position of entry e: w * 16 + e (slot 0 most significant)
