@@ -112,6 +112,16 @@ struct SplitState {
     const int64_t *dims;
     int64_t n_tiles, in_base, t0h, t0m;
     int n_dims, gmask, flags, neg_e;
+    // the power-of-two rescale folded into the last bucket's G table (fold):
+    // G' = G * 2^neg_e, so (G' m0 + G' m1) = (G m0 + G m1) * 2^neg_e bit for
+    // bit while every value stays a normal float (a power-of-two scale
+    // commutes with rounding).  There is no per-tile rescale: 16 v_ldexp per
+    // lane per tile, or even the untaken branch to them, cost 0.2 ms of a
+    // 6.45-ms forward run (profiles/r03_split_fold_ab.jsonl).  Out of the
+    // fold's range (|neg_e| > 32: input maxima far from 1) the rescale is
+    // skipped and the output's exp2 absorbs it; the next bucket renormalises
+    bool fold;
+    float scale;
     int64_t is4[4], isw;          // input stride of slots 0-3; slots 4.. of this wave
     int64_t osl[4], osw;          // output stride of the 4 phase-2 local slots; the wave's other slots
     int32_t glds[F], gsj[F], gsq[F], gsn[F];
@@ -176,6 +186,8 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
         if (d.flags & kScale) e_sum += FBits<float>::exponent(meta[d.in_table[i]].maxbits);
     }
     c.neg_e = (int)(-e_sum);
+    c.fold = (d.flags & kScale) && !(d.flags & kNoFold) && c.neg_e >= -32 && c.neg_e <= 32;
+    c.scale = __builtin_amdgcn_ldexpf(1.0f, c.fold ? c.neg_e : 0);
 }
 
 #ifndef BNPP_DENSE_JR
@@ -191,9 +203,9 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
 #define BNPP_SPLIT_NTL 0      // nontemporal message loads
 #endif
 // timing bisection only (results are wrong with any of these set): drop the
-// power-of-two rescale, the running maximum, the per-tile G offsets
+// running maximum, the per-tile G offsets
 #ifndef BNPP_SPLIT_BISECT
-#define BNPP_SPLIT_BISECT 0   // bit 0 no rescale, bit 1 no maximum, bit 2 G offsets 0
+#define BNPP_SPLIT_BISECT 0   // bit 1 no maximum, bit 2 G offsets 0
 #endif
 #ifndef BNPP_SPLIT_WAVES
 #define BNPP_SPLIT_WAVES 0     // waves per SIMD the register allocation must allow (0: compiler's choice)
@@ -244,7 +256,10 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         cur_begin = d.vblk_begin;
         cur_end = bi + 1 < n_desc ? descs[bi + 1].vblk_begin : total_vblocks;
         split_load_state<F, DEP, DENSE, FORM>(c, d, pool + d.dim_off, meta, w);
-        if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta);
+        // exp2 of the output: the inputs' exp2 and max exponents; a rescale
+        // that is not folded is not applied, so the stored values keep the
+        // inputs' scale and exp2 their exponents only (chain_exp2 + neg_e)
+        if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta) + (c.fold ? 0 : c.neg_e);
         lds_barrier();                                     // the previous bucket's tables are no longer read
         // G_j packed: entry (o, q, n, x) at 8 o + 4 q + 2 n + x holds G_j[o + q
         // gsq + n gsn + x gsj] (gmask is all ones: G_j is input j + 1)
@@ -255,7 +270,8 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             T *dst = small + d.in_lds_off[j + 1];
             for (int e = threadIdx.x; e < span * kSplitPack; e += 64 * W) {
                 const int si = (e >> 3) + ((e >> 2) & 1) * c.gsq[j] + ((e >> 1) & 1) * c.gsn[j] + (e & 1) * c.gsj[j];
-                dst[e] = si < span ? gload(src + si) : T(0);
+                const T g = si < span ? gload(src + si) : T(0);
+                dst[e] = j == F - 1 && c.fold ? g * c.scale : g;
             }
         }
         lds_barrier();
@@ -448,10 +464,8 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             constexpr int j = 4 + decltype(jc)::value;
             split_step<F, 2, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig2);
         });
-        if ((BNPP_SPLIT_BISECT & 1) == 0 && (c.flags & kScale)) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) t[e] = ldexp_t(t[e], c.neg_e);
-        }
+        // (no per-tile rescale: it is folded into G_{F-1}, or, out of the
+        // fold's range, left in the output's exp2 -- see SplitState::fold)
 #pragma unroll
         for (int e = 0; e < 16; ++e)
             if constexpr ((BNPP_SPLIT_BISECT & 2) == 0) lmax = fmaxf(lmax, t[e]);      // entries are >= 0, never NaN
