@@ -323,15 +323,14 @@ def test_split_runs_identical_to_unfused(ctx, capfd, spec):
     partition and tree marginals bit-identical to the one-thread runs of <= 6
     buckets and to one bucket per launch; the plan holds split runs with dense
     addressing (forms 7, 8) and, with BNPP_NO_DENSE, with the general one
-    (forms 5, 6) -- both bit-identical; the rescale folded into the last G
-    table or (BNPP_SPLIT_NOFOLD) left in the output's exponent, too."""
+    (forms 5, 6) -- both bit-identical (the split runs fold their rescale
+    into the last G table)."""
     r, c, ev = spec
     ev = ev or {}
     m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=13))
     col = [i * c + j for j in range(c) for i in range(r)]
     knobs = [{"BNPP_DEBUG_CHAIN": "1"}, {"BNPP_DEBUG_CHAIN": "1", "BNPP_NO_DENSE": "1"}, {"BNPP_SPLIT_MIN_F": "7"},
-             {"BNPP_NO_SPLIT": "1"}, {"BNPP_NO_SPLIT": "1", "BNPP_CHAIN_RUN_MAX": "6"}, {"BNPP_NO_CHAIN": "1"},
-             {"BNPP_SPLIT_NOFOLD": "1"}]
+             {"BNPP_NO_SPLIT": "1"}, {"BNPP_NO_SPLIT": "1", "BNPP_CHAIN_RUN_MAX": "6"}, {"BNPP_NO_CHAIN": "1"}]
     res = []
     for kn in knobs:
         os.environ.update(kn)
