@@ -66,16 +66,30 @@ std::vector<int> cards_of(std::initializer_list<const Domain *> ds) {
     return c;
 }
 
+// sum in linear order from 0.0 (a VE result's last op is a product,
+// model.cpp:423/437; a loaded table's sum as io.cpp reads it)
 double seq_sum(const std::vector<double> &v) {
     double p = 0;
     for (double x : v) p += x;
     return p;
 }
 
-std::vector<double> download(const DevBuf &b, uint64_t n) {
-    std::vector<double> v(n);
+// an output table plus one trailing double for the op's partition sum
+// (bnpp.h out_sum), downloaded together
+struct OutBuf : DevBuf {
+    uint64_t n;
+    explicit OutBuf(uint64_t n_) : DevBuf((std::max<uint64_t>(n_, 1) + 1) * sizeof(double)), n(n_) {}
+    double *sum() const { return static_cast<double *>(p) + std::max<uint64_t>(n, 1); }
+};
+
+// the table and the reference's running sum (Factor::_partition) computed
+// on the device in the reference's order (factor.cpp:139, 172, 208, 236)
+std::vector<double> download(const OutBuf &b, double &partition) {
+    std::vector<double> v(std::max<uint64_t>(b.n, 1) + 1);
     check(bnpp_synchronize(ctx(), nullptr), "synchronize");
-    check(bnpp_memcpy_d2h(ctx(), v.data(), b.p, n * sizeof(double)), "memcpy d2h");
+    check(bnpp_memcpy_d2h(ctx(), v.data(), b.p, v.size() * sizeof(double)), "memcpy d2h");
+    partition = v.back();
+    v.resize(b.n);
     return v;
 }
 
@@ -218,13 +232,13 @@ Factor Factor::product(const Factor &f) const {
     Domain *nd = new Domain(*_domain, *f._domain);
     std::vector<int> cards = cards_of({_domain, f._domain});
     auto a = upload(_values), b = upload(f._values);
-    DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
+    OutBuf out(nd->size());
     std::vector<int> av = ids(*_domain), bv = ids(*f._domain), ov = ids(*nd);
     check(bnpp_product(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
-                       bv.data(), out.p, (int)ov.size(), ov.data()),
+                       bv.data(), out.p, (int)ov.size(), ov.data(), out.sum()),
           "product");
-    std::vector<double> vals = download(out, nd->size());
-    double p = seq_sum(vals);
+    double p = 0;
+    std::vector<double> vals = download(out, p);
     return Factor(nd, std::move(vals), p);
 }
 
@@ -232,13 +246,13 @@ Factor Factor::divide(const Factor &f) const {
     Domain *nd = new Domain(*_domain, *f._domain);                 // same scope rule as product
     std::vector<int> cards = cards_of({_domain, f._domain});
     auto a = upload(_values), b = upload(f._values);
-    DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
+    OutBuf out(nd->size());
     std::vector<int> av = ids(*_domain), bv = ids(*f._domain), ov = ids(*nd);
     check(bnpp_divide(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
-                      bv.data(), out.p, (int)ov.size(), ov.data()),
+                      bv.data(), out.p, (int)ov.size(), ov.data(), out.sum()),
           "divide");
-    std::vector<double> vals = download(out, nd->size());
-    double p = seq_sum(vals);
+    double p = 0;
+    std::vector<double> vals = download(out, p);
     return Factor(nd, std::move(vals), p);
 }
 
@@ -247,13 +261,13 @@ Factor Factor::sum_out(const Variable *variable) const {
     Domain *nd = new Domain(*_domain, variable);
     std::vector<int> cards = cards_of({_domain});
     auto a = upload(_values);
-    DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
+    OutBuf out(nd->size());
     std::vector<int> av = ids(*_domain), ov = ids(*nd);
     check(bnpp_sum_out(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), (int)variable->id(),
-                       out.p, (int)ov.size(), ov.data()),
+                       out.p, (int)ov.size(), ov.data(), out.sum()),
           "sum_out");
-    std::vector<double> vals = download(out, nd->size());
-    double p = seq_sum(vals);
+    double p = 0;
+    std::vector<double> vals = download(out, p);
     return Factor(nd, std::move(vals), p);
 }
 
@@ -266,13 +280,13 @@ Factor Factor::conditioning(const std::unordered_map<unsigned, unsigned> &eviden
         ev_vals.push_back((int)kv.second);
     }
     auto a = upload(_values);
-    DevBuf out(std::max<uint64_t>(nd->size(), 1) * sizeof(double));
+    OutBuf out(nd->size());
     std::vector<int> av = ids(*_domain);
     check(bnpp_condition(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), (int)ev_vars.size(),
-                         ev_vars.data(), ev_vals.data(), out.p),
+                         ev_vars.data(), ev_vals.data(), out.p, out.sum()),
           "conditioning");
-    std::vector<double> vals = download(out, nd->size());
-    double p = seq_sum(vals);
+    double p = 0;
+    std::vector<double> vals = download(out, p);
     return Factor(nd, std::move(vals), p);
 }
 
@@ -482,7 +496,34 @@ Factor BN::query_ve(const std::unordered_set<const Variable *> &target,
 }
 
 MN::MN(std::string name, std::vector<Variable *> &variables, std::vector<Factor *> &factors)
-    : Model(std::move(name), variables, factors) {}
+    : Model(std::move(name), variables, factors) {
+    for (auto pv : _variables) _neighbors[pv];                     // model.cpp:962-977
+    for (auto pf : _factors) {
+        const std::vector<const Variable *> &scope = pf->domain().scope();
+        for (auto pv1 : scope)
+            for (auto pv2 : scope)
+                if (pv1->id() != pv2->id()) _neighbors[pv1].insert(pv2);
+    }
+}
+
+void MN::write(std::ostream &os) const {                            // model.cpp:979-999
+    os << "MARKOV:" << std::endl;
+    os << ">> Variables" << std::endl;
+    for (auto pv1 : _variables) {
+        os << *pv1 << ", ";
+        os << "neighbors:{";
+        for (auto pv2 : _neighbors.find(pv1)->second) os << " " << pv2->id();
+        os << " }" << std::endl;
+    }
+    os << std::endl;
+    os << ">> Factors" << std::endl;
+    for (auto pf : _factors) os << *pf << std::endl;
+}
+
+std::ostream &operator<<(std::ostream &os, const MN &mn) {
+    mn.write(os);
+    return os;
+}
 
 // -------------------------------------------------------------------- I/O
 namespace {

@@ -49,7 +49,6 @@ enum BucketFlags : int32_t {
     kOutStrided = 4,   // dims permuted: output offset from per-dim output strides
                        // (n_dims words after the dims rows in the pool)
     kDivide = 16,      // Factor::divide (factor.cpp:149-180): p = in_0 / in_1 instead of the product
-    kNoFold = 32,      // split runs: leave the rescale in the output's exp2 (test knob BNPP_SPLIT_NOFOLD)
     kChainLo32 = 8,    // chain form: the streamed side (forward input / backward output)
                        // is linear in the thread index, so one wave's accesses are a
                        // uniform base + a 32-bit lane offset (saddr addressing)

@@ -56,7 +56,9 @@ int main(int argc, char **argv) {
         delete model;
         return -2;
     }
-    if (options["verbose"]) {
+    if (options["verbose"]) {                          // mn.cpp:96-106
+        std::cout << ">> Model:" << std::endl;
+        std::cout << *model << std::endl;
         std::cout << ">> Evidence:" << std::endl;
         for (auto &kv : evidence) std::cout << "Variable = " << kv.first << ", Value = " << kv.second << std::endl;
         std::cout << std::endl;

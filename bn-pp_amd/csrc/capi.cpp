@@ -125,6 +125,45 @@ int run_single(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &c
     return BNPP_OK;
 }
 
+// Factor::_partition of a single-op call (seqsum.hip), enqueued after the op
+// on the same stream: the terms of the inputs' chain product (or in[0] /
+// in[1]) over `dims` -- the reference's output scope order, last fastest --
+// with elim_var's values inner, added one at a time in that order.
+int run_seq_sum(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &cards, const std::vector<View> &in,
+                const std::vector<const void *> &ptrs, const std::vector<int> &dims, int elim_var, bool divide,
+                double *out_sum) {
+    if (!out_sum) return BNPP_OK;
+    if (dims.size() > (size_t)kSeqMaxDims || in.size() > (size_t)kMaxIn)
+        return set_err(BNPP_ERR_UNSUPPORTED, "out_sum: at most 32 output variables");
+    SeqSumArgs a;
+    std::memset(&a, 0, sizeof a);
+    const int64_t eb = dtype == BNPP_F32 ? 4 : 8;
+    bool has_elim = false;
+    for (const View &v : in)
+        for (int x : v.vars) has_elim = has_elim || (elim_var >= 0 && x == elim_var);
+    a.k = has_elim ? cards[elim_var] : 1;
+    a.n_terms = a.k;
+    for (int x : dims) a.n_terms = sat_mul(a.n_terms, cards[x]);
+    a.n_in = (int)in.size();
+    a.n_dims = (int)dims.size();
+    a.divide = divide ? 1 : 0;
+    a.out = out_sum;
+    for (size_t d = 0; d < dims.size(); ++d) a.card[d] = cards[dims[d]];
+    for (size_t n = 0; n < in.size(); ++n) {
+        a.in[n] = static_cast<const unsigned char *>(ptrs[n]) + in[n].base * eb;
+        for (size_t j = 0; j < in[n].vars.size(); ++j) {
+            const int x = in[n].vars[j];
+            if (has_elim && x == elim_var) a.stride[n][kSeqMaxDims] = in[n].strides[j];
+            for (size_t d = 0; d < dims.size(); ++d)
+                if (dims[d] == x) a.stride[n][d] = in[n].strides[j];
+        }
+    }
+    hipError_t e = hipSetDevice(ctx->c.device);
+    if (e == hipSuccess) e = launch_seq_sum(dtype == BNPP_F32, a, pick_stream(ctx, stream));
+    if (e != hipSuccess) return set_err(BNPP_ERR_HIP, std::string("partition sum launch: ") + hipGetErrorString(e));
+    return BNPP_OK;
+}
+
 // evidence as a per-variable array (-1: none); validates ids and values
 bool evidence_array(const ModelData &d, int n_ev, const int *ev_vars, const int *ev_vals, std::vector<int> &ev,
                     std::string &msg) {
@@ -809,7 +848,7 @@ int bnpp_out_scope(int n_in, const int *in_ndims, const int *const *in_vars, int
 
 int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, int n_in,
                           const void *const *in_tables, const int *in_ndims, const int *const *in_vars, int elim_var,
-                          void *out_table, int out_ndims, const int *out_vars) {
+                          void *out_table, int out_ndims, const int *out_vars, double *out_sum) {
     BNPP_GUARD_BEGIN
     if (!ctx || !cards || n_in < 1 || !in_tables || !in_ndims || !in_vars || !out_table)
         return set_err(BNPP_ERR_INVALID, "null argument");
@@ -837,22 +876,25 @@ int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, c
     if (us != os) return set_err(BNPP_ERR_INVALID, "output scope must be the union of the inputs minus elim_var");
     b.out_vars = ov;
     b.out_table = n_in;
-    return run_single(ctx, stream, dtype, cv, b, ptrs, out_table);
+    int rc = run_single(ctx, stream, dtype, cv, b, ptrs, out_table);
+    if (rc == BNPP_OK) rc = run_seq_sum(ctx, stream, dtype, cv, b.in, ptrs, u, elim_var, false, out_sum);
+    return rc;
     BNPP_GUARD_END
 }
 
 int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *a, int a_ndims,
                  const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
-                 const int *out_vars) {
+                 const int *out_vars, double *out_sum) {
     const void *tabs[2] = {a, b};
     const int nd[2] = {a_ndims, b_ndims};
     const int *vs[2] = {a_vars, b_vars};
-    return bnpp_bucket_eliminate(ctx, stream, dtype, n_cards, cards, 2, tabs, nd, vs, -1, out, out_ndims, out_vars);
+    return bnpp_bucket_eliminate(ctx, stream, dtype, n_cards, cards, 2, tabs, nd, vs, -1, out, out_ndims, out_vars,
+                                 out_sum);
 }
 
 int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *a, int a_ndims,
                 const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
-                const int *out_vars) {
+                const int *out_vars, double *out_sum) {
     BNPP_GUARD_BEGIN
     if (!ctx || !cards || !a || !b || !out || (a_ndims > 0 && !a_vars) || (b_ndims > 0 && !b_vars) ||
         (out_ndims > 0 && !out_vars))
@@ -871,18 +913,21 @@ int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *
     bs.out_vars = ov;
     bs.out_table = 2;
     bs.divide = true;
-    return run_single(ctx, stream, dtype, cv, bs, {a, b}, out);
+    int rc = run_single(ctx, stream, dtype, cv, bs, {a, b}, out);
+    if (rc == BNPP_OK) rc = run_seq_sum(ctx, stream, dtype, cv, bs.in, {a, b}, u, -1, true, out_sum);
+    return rc;
     BNPP_GUARD_END
 }
 
 int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *in, int ndims,
-                 const int *vars, int var, void *out, int out_ndims, const int *out_vars) {
+                 const int *vars, int var, void *out, int out_ndims, const int *out_vars, double *out_sum) {
     const void *tabs[1] = {in};
-    return bnpp_bucket_eliminate(ctx, stream, dtype, n_cards, cards, 1, tabs, &ndims, &vars, var, out, out_ndims, out_vars);
+    return bnpp_bucket_eliminate(ctx, stream, dtype, n_cards, cards, 1, tabs, &ndims, &vars, var, out, out_ndims, out_vars,
+                                 out_sum);
 }
 
 int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *in, int ndims,
-                   const int *vars, int n_ev, const int *ev_vars, const int *ev_vals, void *out) {
+                   const int *vars, int n_ev, const int *ev_vars, const int *ev_vals, void *out, double *out_sum) {
     BNPP_GUARD_BEGIN
     if (!ctx || !cards || !in || !out || (ndims > 0 && !vars) || n_ev < 0 || (n_ev > 0 && (!ev_vars || !ev_vals)))
         return set_err(BNPP_ERR_INVALID, "null argument");
@@ -901,7 +946,9 @@ int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const in
     b.in.push_back(conditioned_view(0, s, cv, ev));
     b.out_vars = b.in[0].vars;
     b.out_table = 1;
-    return run_single(ctx, stream, dtype, cv, b, {in}, out);
+    int rc = run_single(ctx, stream, dtype, cv, b, {in}, out);
+    if (rc == BNPP_OK) rc = run_seq_sum(ctx, stream, dtype, cv, b.in, {in}, b.out_vars, -1, false, out_sum);
+    return rc;
     BNPP_GUARD_END
 }
 

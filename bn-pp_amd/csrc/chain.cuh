@@ -12,8 +12,8 @@
 // F buckets on them in registers -- each in the reference's arithmetic order,
 // p = G_q * msg, acc = 0; acc += p for x_q = 0..K-1 (factor.cpp:131-143,
 // 199-205) -- and writes the run's output once: HBM traffic per bucket / F.
-// The intermediate messages are exactly the unfused ones (up to the power-of-
-// two scale, which is applied once at the end), so fp64 stays bit-identical.
+// The intermediate messages are exactly the unfused ones up to a power-of-two
+// scale (folded into the G tables, chain_fold), so fp64 stays bit-identical.
 #pragma once
 #include <type_traits>
 #include <utility>
@@ -99,20 +99,7 @@ __device__ __forceinline__ void chain_load_state(ChainState<F> &c, const BucketD
     }
     c.big = meta[d.in_table[0]].ptr;
     c.out = meta[d.out_table].ptr;
-    int64_t e_sum = 0, x_sum = 0;
-    for (int i = 0; i < kMaxDescIn; ++i) {
-        if (i >= d.n_in) break;
-        const TableMeta &mi = meta[d.in_table[i]];
-        const int e = FBits<T>::exponent(mi.maxbits);
-        if (d.flags & kScale) {
-            e_sum += e;
-            x_sum += mi.exp2 + e;
-        } else {
-            x_sum += mi.exp2;
-        }
-    }
-    c.neg_e = (int)(-e_sum);
-    (void)x_sum;
+    c.neg_e = 0;                                           // chain_stage: the share not folded into G
 }
 
 template <typename T>
@@ -126,17 +113,50 @@ __device__ __forceinline__ int64_t chain_exp2(const BucketDesc &d, TableMeta *me
     return x_sum;
 }
 
-// copy the G tables of the run into LDS (uniform control flow)
+// A run's power-of-two rescale, folded into its G tables as they are staged
+// in LDS.  Input i >= 1 (a G table) is staged as G * 2^s[i] with s[i] = -(its
+// max exponent); the first one also takes -(the incoming message's, input 0).
+// Every bucket's output then differs from the unfused bucket's (rescaled by
+// its inputs' max exponents, kernels.cuh) by one power of two common to all
+// its entries, so intermediate values stay where one bucket per launch keeps
+// them (normal floats, however peaked the potentials) and the results are
+// bit-identical to it: a power-of-two scale commutes with IEEE rounding.  A
+// share beyond +-cap (maxima far outside the normal range) carries into the
+// next table; the return value is what is left after the last one, for the
+// output (applied by the one-thread runs, kept in exp2 by the split runs).
 template <typename T>
-__device__ __forceinline__ void chain_stage(const BucketDesc &d, TableMeta *meta, T *small) {
+__device__ __forceinline__ int chain_fold(const BucketDesc &d, const TableMeta *meta, int (&s)[kMaxDescIn]) {
+    constexpr int cap = sizeof(T) == 4 ? 120 : 1000;
+    int carry = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxDescIn; ++i) {
+        s[i] = 0;
+        if (i >= d.n_in || !(d.flags & kScale)) continue;
+        carry -= FBits<T>::exponent(meta[d.in_table[i]].maxbits);
+        if (i == 0) continue;
+        s[i] = carry > cap ? cap : carry < -cap ? -cap : carry;
+        carry -= s[i];
+    }
+    return carry;
+}
+
+// copy the G tables of the run into LDS, scaled by chain_fold's shares
+// (uniform control flow); returns the share left for the output
+template <typename T>
+__device__ __forceinline__ int chain_stage(const BucketDesc &d, TableMeta *meta, T *small) {
+    int s[kMaxDescIn];
+    const int left = chain_fold<T>(d, meta, s);
     __syncthreads();
+#pragma unroll
     for (int i = 1; i < kMaxDescIn; ++i) {
         if (i >= d.n_in) break;
         const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
         const int off = d.in_lds_off[i], span = d.in_span[i];
-        for (int e = threadIdx.x; e < span; e += kBlock) small[off + e] = gload(src + e);
+        const T sc = ldexp_t(T(1), s[i]);
+        for (int e = threadIdx.x; e < span; e += kBlock) small[off + e] = gload(src + e) * sc;
     }
     __syncthreads();
+    return left;
 }
 
 // Bucket J of a run on the register table t (MODE 0: no factor tables,
@@ -301,7 +321,7 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
             cur_begin = d.vblk_begin;
             chain_load_state<T, K, F, FORM>(c, d, pool + d.dim_off, meta);
             if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta);
-            chain_stage<T>(d, meta, small);
+            c.neg_e = chain_stage<T>(d, meta, small);      // the rescale is in the G tables but this share
         }
         const int64_t tid0 = (vb - cur_begin) * kBlock;
         const int64_t tid = tid0 + threadIdx.x;
@@ -383,7 +403,7 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                     chain_step<T, K, F, V, j, 1, DEP, SUM>(t, small, gb[j], c.gs[j], c.gsn[j]);
             });
             constexpr int NOUT = SUM ? 1 : N;                   // live entries (summing run: t[0])
-            if (c.flags & kScale) {
+            if (c.neg_e != 0) {                                 // uniform; 0 unless maxima leave the fold's range
 #pragma unroll
                 for (int a = 0; a < NOUT; ++a)
 #pragma unroll

@@ -111,17 +111,14 @@ struct SplitState {
     float *out;
     const int64_t *dims;
     int64_t n_tiles, in_base, t0h, t0m;
-    int n_dims, gmask, flags, neg_e;
-    // the power-of-two rescale folded into the last bucket's G table (fold):
-    // G' = G * 2^neg_e, so (G' m0 + G' m1) = (G m0 + G m1) * 2^neg_e bit for
-    // bit while every value stays a normal float (a power-of-two scale
-    // commutes with rounding).  There is no per-tile rescale: 16 v_ldexp per
-    // lane per tile, or even the untaken branch to them, cost 0.2 ms of a
-    // 6.45-ms forward run (profiles/r03_split_fold_ab.jsonl).  Out of the
-    // fold's range (|neg_e| > 32: input maxima far from 1) the rescale is
-    // skipped and the output's exp2 absorbs it; the next bucket renormalises
-    bool fold;
-    float scale;
+    // the power-of-two rescale is folded into the G tables as they are staged
+    // (chain_fold: G_j' = G_j * 2^s_j, every bucket's output scaled as the
+    // unfused bucket's); there is no per-tile rescale: 16 v_ldexp per lane per
+    // tile, or even the untaken branch to them, cost 0.2 ms of a 6.45-ms
+    // forward run (profiles/r03_split_fold_ab.jsonl).  left: the share past
+    // the fold's range (never, unless maxima leave the normal range), kept in
+    // the output's exp2
+    int n_dims, gmask, flags, left;
     int64_t is4[4], isw;          // input stride of slots 0-3; slots 4.. of this wave
     int64_t osl[4], osw;          // output stride of the 4 phase-2 local slots; the wave's other slots
     int32_t glds[F], gsj[F], gsq[F], gsn[F];
@@ -180,14 +177,7 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
     }
     c.big = static_cast<const float *>(meta[d.in_table[0]].ptr);
     c.out = static_cast<float *>(meta[d.out_table].ptr);
-    int64_t e_sum = 0;
-    for (int i = 0; i < kMaxDescIn; ++i) {
-        if (i >= d.n_in) break;
-        if (d.flags & kScale) e_sum += FBits<float>::exponent(meta[d.in_table[i]].maxbits);
-    }
-    c.neg_e = (int)(-e_sum);
-    c.fold = (d.flags & kScale) && !(d.flags & kNoFold) && c.neg_e >= -32 && c.neg_e <= 32;
-    c.scale = __builtin_amdgcn_ldexpf(1.0f, c.fold ? c.neg_e : 0);
+    c.left = 0;
 }
 
 #ifndef BNPP_DENSE_JR
@@ -256,22 +246,24 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         cur_begin = d.vblk_begin;
         cur_end = bi + 1 < n_desc ? descs[bi + 1].vblk_begin : total_vblocks;
         split_load_state<F, DEP, DENSE, FORM>(c, d, pool + d.dim_off, meta, w);
-        // exp2 of the output: the inputs' exp2 and max exponents; a rescale
-        // that is not folded is not applied, so the stored values keep the
-        // inputs' scale and exp2 their exponents only (chain_exp2 + neg_e)
-        if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta) + (c.fold ? 0 : c.neg_e);
+        int fs[kMaxDescIn];
+        c.left = chain_fold<T>(d, meta, fs);
+        // exp2 of the output: the inputs' exp2 and max exponents, plus the
+        // share of the rescale not folded (chain_fold)
+        if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta) + c.left;
         lds_barrier();                                     // the previous bucket's tables are no longer read
         // G_j packed: entry (o, q, n, x) at 8 o + 4 q + 2 n + x holds G_j[o + q
-        // gsq + n gsn + x gsj] (gmask is all ones: G_j is input j + 1)
+        // gsq + n gsn + x gsj] * 2^fs (gmask is all ones: G_j is input j + 1)
 #pragma unroll
         for (int j = 0; j < F; ++j) {
             const T *src = static_cast<const T *>(meta[d.in_table[j + 1]].ptr) + d.in_base[j + 1];
             const int span = d.in_span[j + 1];
             T *dst = small + d.in_lds_off[j + 1];
+            const T sc = __builtin_amdgcn_ldexpf(1.0f, fs[j + 1]);
             for (int e = threadIdx.x; e < span * kSplitPack; e += 64 * W) {
                 const int si = (e >> 3) + ((e >> 2) & 1) * c.gsq[j] + ((e >> 1) & 1) * c.gsn[j] + (e & 1) * c.gsj[j];
                 const T g = si < span ? gload(src + si) : T(0);
-                dst[e] = j == F - 1 && c.fold ? g * c.scale : g;
+                dst[e] = g * sc;
             }
         }
         lds_barrier();
@@ -464,8 +456,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             constexpr int j = 4 + decltype(jc)::value;
             split_step<F, 2, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig2);
         });
-        // (no per-tile rescale: it is folded into G_{F-1}, or, out of the
-        // fold's range, left in the output's exp2 -- see SplitState::fold)
+        // (no per-tile rescale: it is folded into the G tables, SplitState)
 #pragma unroll
         for (int e = 0; e < 16; ++e)
             if constexpr ((BNPP_SPLIT_BISECT & 2) == 0) lmax = fmaxf(lmax, t[e]);      // entries are >= 0, never NaN

@@ -412,7 +412,6 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     d.flags = kScale | kTrackMax;
     d.big = -1;
     d.chain = F | (b.chain_gmask << 8) | (form << 16) | (dep << 20);
-    if (chain_split_form(form) && std::getenv("BNPP_SPLIT_NOFOLD")) d.flags |= kNoFold;
     {
         // the streamed side linear in the thread index: a wave spans 64 * V
         // consecutive rest entries -> uniform base + 32-bit lane byte offset

@@ -31,6 +31,20 @@ struct SingleArgs {
     int64_t pool[kMaxPool];
 };
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream);
+// the reference's running sum of a single-op call (seqsum.hip): the terms
+// prod_n in[n][pos_n(i, val)] (or in[0] / in[1]) for i over the output dims
+// (reference scope order, last fastest) and val < k inner, added in order
+constexpr int kSeqMaxDims = 32;
+struct SeqSumArgs {
+    const void *in[kMaxIn];                        // input tables, base offsets applied
+    double *out;                                   // device
+    int64_t n_terms;                               // output entries * k
+    int64_t k;                                     // card of the summed variable (1: none)
+    int n_in, n_dims, divide, pad;
+    int64_t card[kSeqMaxDims];
+    int64_t stride[kMaxIn][kSeqMaxDims + 1];       // per input: on each output dim, then on the summed variable
+};
+hipError_t launch_seq_sum(bool f32, const SeqSumArgs &a, hipStream_t stream);
 // message exchange steps of sliced runs (xchg.hip; plan.hpp BucketSpec::xchg)
 hipError_t launch_xchg_sync(bool f32, TableMeta *meta, int in_t, int x_t, int R, hipStream_t s);
 hipError_t launch_xchg_pack(bool f32, TableMeta *meta, int in_t, int x_t, int out_t, int R, int mode, int64_t n,

@@ -57,11 +57,11 @@ _SIGS = {
     "bnpp_memcpy_d2h": (_I, [_P, _P, _P, C.c_size_t]),
     "bnpp_synchronize": (_I, [_P, _P]),
     "bnpp_out_scope": (_I, [_I, _IP, C.POINTER(_IP), _I, _I, _IP, _IP]),
-    "bnpp_bucket_eliminate": (_I, [_P, _P, _I, _I, _IP, _I, C.POINTER(_P), _IP, C.POINTER(_IP), _I, _P, _I, _IP]),
-    "bnpp_product": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP]),
-    "bnpp_divide": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP]),
-    "bnpp_sum_out": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _I, _P, _I, _IP]),
-    "bnpp_condition": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _I, _IP, _IP, _P]),
+    "bnpp_bucket_eliminate": (_I, [_P, _P, _I, _I, _IP, _I, C.POINTER(_P), _IP, C.POINTER(_IP), _I, _P, _I, _IP, _P]),
+    "bnpp_product": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P]),
+    "bnpp_divide": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P, _I, _IP, _P]),
+    "bnpp_sum_out": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _I, _P, _I, _IP, _P]),
+    "bnpp_condition": (_I, [_P, _P, _I, _I, _IP, _P, _I, _IP, _I, _IP, _IP, _P, _P]),
     "bnpp_model_load_uai": (_I, [C.c_char_p, C.POINTER(_P)]),
     "bnpp_model_from_arrays": (_I, [_I, _I, _IP, _I, _IP, _IP, _DP, C.POINTER(_P)]),
     "bnpp_model_free": (_I, [_P]),
@@ -97,7 +97,7 @@ EXPORTED = sorted(_SIGS)
 
 # The signature table above is for this ABI version (include/bnpp.h
 # BNPP_VERSION); a library of another version would take shifted arguments.
-ABI_VERSION = 201
+ABI_VERSION = 202
 if _lib.bnpp_version() != ABI_VERSION:
     raise ImportError("libbnpp.so ABI version %d, this binding expects %d (%s)"
                       % (_lib.bnpp_version(), ABI_VERSION, LIB_PATH))
@@ -512,28 +512,30 @@ class Job:
 
 def bucket_eliminate(ctx: Context, dtype: int, cards: Sequence[int], tables: Sequence[int],
                      scopes: Sequence[Sequence[int]], elim: int, out: int, out_vars: Sequence[int],
-                     stream: Optional[int] = None) -> None:
+                     stream: Optional[int] = None, out_sum: Optional[int] = None) -> None:
     """Fused bucket on caller-owned device buffers (addresses as ints, e.g. torch
-    tensor.data_ptr()).  Only enqueues on `stream`."""
+    tensor.data_ptr()).  Only enqueues on `stream`.  out_sum: device address of
+    a float64 that receives the reference's partition sum (include/bnpp.h)."""
     arrs = [_ints(s) for s in scopes]
     ptrs = (_IP * len(arrs))(*[C.cast(a, _IP) for a in arrs])
     tabs = (_P * len(tables))(*[_P(t) for t in tables])
     _check(_lib.bnpp_bucket_eliminate(ctx.handle, _P(stream) if stream else None, dtype, len(cards), _ints(cards), len(tables),
                                       tabs, _ints([len(s) for s in scopes]), ptrs, elim, _P(out), len(out_vars),
-                                      _ints(out_vars)), "bnpp_bucket_eliminate")
+                                      _ints(out_vars), _P(out_sum) if out_sum else None), "bnpp_bucket_eliminate")
 
 
 def divide(ctx: Context, dtype: int, cards: Sequence[int], a: int, a_scope: Sequence[int], b: int,
-           b_scope: Sequence[int], out: int, out_vars: Sequence[int], stream: Optional[int] = None) -> None:
+           b_scope: Sequence[int], out: int, out_vars: Sequence[int], stream: Optional[int] = None,
+           out_sum: Optional[int] = None) -> None:
     """Factor::divide (factor.cpp:149-180) on caller-owned device buffers:
     out = a / b over the union scope (out_vars in any order of it)."""
     _check(_lib.bnpp_divide(ctx.handle, _P(stream) if stream else None, dtype, len(cards), _ints(cards), _P(a), len(a_scope),
                             _ints(a_scope), _P(b), len(b_scope), _ints(b_scope), _P(out), len(out_vars),
-                            _ints(out_vars)), "bnpp_divide")
+                            _ints(out_vars), _P(out_sum) if out_sum else None), "bnpp_divide")
 
 
 def condition(ctx: Context, dtype: int, cards: Sequence[int], table: int, scope: Sequence[int],
-              evidence: Dict[int, int], out: int, stream: Optional[int] = None) -> None:
+              evidence: Dict[int, int], out: int, stream: Optional[int] = None, out_sum: Optional[int] = None) -> None:
     n, ev_v, ev_x = _ev(evidence)
     _check(_lib.bnpp_condition(ctx.handle, _P(stream) if stream else None, dtype, len(cards), _ints(cards), _P(table), len(scope),
-                               _ints(scope), n, ev_v, ev_x, _P(out)), "bnpp_condition")
+                               _ints(scope), n, ev_v, ev_x, _P(out), _P(out_sum) if out_sum else None), "bnpp_condition")

@@ -128,7 +128,18 @@ class TorchCollective:
     tensors (CUDA array interface) and the collective runs on the engine's
     stream (ExternalStream), so RCCL orders itself after the pack kernel and
     the next kernel after RCCL.  gloo (tests, CPU): the engine's stream is
-    synchronised, the bytes staged through host memory."""
+    synchronised, the bytes staged through host memory.
+
+    nccl process groups: one per lane of a two-front schedule (the lanes
+    exchange concurrently, each on its own communicator).  They are created,
+    and their communicators initialised by one tiny all-reduce, here -- before
+    the engine runs -- never from inside the engine's launch loop; a lane's
+    stream is bound to the next unused group at its first exchange, which
+    every rank reaches in the same order.  Build one per (context, world) and
+    reuse it (sliced_tree_marginals caches it on the context): groups and
+    communicators live as long as it does."""
+
+    LANES = 2
 
     def __init__(self, ctx, dist, world: int, timeout_s: float = 0):
         import bnpp
@@ -136,12 +147,23 @@ class TorchCollective:
         self.backend = dist.get_backend() if dist is not None and dist.is_initialized() else "gloo"
         self.calls = 0
         self.bytes_sent = 0
-        # nccl: one process group per engine stream (the two lanes of a
-        # two-front schedule exchange concurrently, each on its own
-        # communicator); created at a lane's first exchange, which every rank
-        # reaches in the same order
-        self.groups = {}
+        self.groups = {}               # engine stream -> process group
+        self.pool = []
         self.timeout_s = timeout_s
+        if self.backend == "nccl":
+            import datetime
+            import torch
+            kw = {"timeout": datetime.timedelta(seconds=timeout_s)} if timeout_s > 0 else {}
+            for _ in range(self.LANES):
+                g = dist.new_group(backend="nccl", **kw)
+                t = torch.zeros(1, device="cuda")
+                dist.all_reduce(t, group=g)          # the communicator is set up now, not mid-run
+                self.pool.append(g)
+            torch.cuda.synchronize()
+
+    def reset_stats(self):
+        self.calls = 0
+        self.bytes_sent = 0
 
     def _host(self, ptr: int, nbytes: int):
         import numpy as np
@@ -168,12 +190,9 @@ class TorchCollective:
         self.bytes_sent += nbytes * (R - 1)
         if self.backend == "nccl":
             if stream not in self.groups:
-                if self.timeout_s > 0:
-                    import datetime
-                    self.groups[stream] = self.dist.new_group(backend="nccl",
-                                                              timeout=datetime.timedelta(seconds=self.timeout_s))
-                else:
-                    self.groups[stream] = self.dist.new_group(backend="nccl")
+                if len(self.groups) >= len(self.pool):
+                    raise RuntimeError("sliced run: more engine streams than prepared process groups")
+                self.groups[stream] = self.pool[len(self.groups)]
             grp = self.groups[stream]
             s = torch.cuda.ExternalStream(stream)
             with torch.cuda.stream(s):
@@ -193,6 +212,18 @@ class TorchCollective:
             self.dist.all_to_all_single(rt, st)
         arr = rt.numpy()
         bnpp._check(bnpp._lib.bnpp_memcpy_h2d(self.ctx.handle, recv, arr.ctypes.data, nbytes * R), "h2d")
+
+
+def collective_for(ctx, dist, world: int, timeout_s: float = 0) -> TorchCollective:
+    """The context's TorchCollective for this world (created once: its nccl
+    groups and communicators are reused by every later sliced call)."""
+    key = (id(dist), world, timeout_s)
+    coll = getattr(ctx, "_sliced_coll", None)
+    if coll is None or getattr(ctx, "_sliced_coll_key", None) != key:
+        coll = TorchCollective(ctx, dist, world, timeout_s)
+        ctx._sliced_coll, ctx._sliced_coll_key = coll, key
+    coll.reset_stats()
+    return coll
 
 
 def combine_shares(n_vars: int, cards: Sequence[int], mant: Dict[int, List[float]], exps: Dict[int, int],
@@ -254,7 +285,7 @@ def sliced_tree_marginals(ctx, model, rank: int, world: int, dist=None, evidence
     (bnpp_marginals_tree_sliced): -> ({var: marginal}, collective stats)."""
     import bnpp
 
-    coll = TorchCollective(ctx, dist, world, timeout_s)
+    coll = collective_for(ctx, dist, world, timeout_s)
     if not getattr(ctx, "_sliced_trimmed", False):
         # the first sliced call on this context: what it cached for other
         # calls (e.g. a segment-scheme arena) is freed, so the budget below

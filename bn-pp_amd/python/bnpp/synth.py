@@ -40,6 +40,33 @@ def ising_grid(rows: int, cols: int, seed: int = 0) -> dict:
     return {"type": "MARKOV", "cards": [2] * n, "scopes": scopes, "values": values}
 
 
+def peaked_grid(rows: int, cols: int, log2_eps: int = 10, seed: int = 0) -> dict:
+    """R x C binary grid whose bucket products peak far below 1 (the factor
+    list as ising_grid's).  unary = [a, eps b] prefers x = 0, the vertical pair
+    (v, v+C) = [eps c, eps d, e, f] penalises x_v = 0, the horizontal pair is
+    U(0.5, 1): on a column sweep the bucket of every variable above the last
+    row holds all three, so its product is <= eps everywhere (eps = 2^-log2_eps)
+    although every table's maximum is near 1 -- a run of F fused buckets then
+    carries a power-of-two rescale of about F * log2_eps."""
+    rng = random.Random(seed)
+    eps = 2.0 ** -log2_eps
+    u = lambda: rng.uniform(0.5, 1.0)
+    n = rows * cols
+    scopes, values = [], []
+    for i in range(n):
+        scopes.append([i])
+        values.append([_r6(u()), _r6(eps * u())])
+    pairs = [(r * cols + c, r * cols + c + 1) for r in range(rows) for c in range(cols - 1)]
+    for a, b in pairs:
+        scopes.append([a, b])
+        values.append([_r6(u()) for _ in range(4)])
+    vpairs = [(r * cols + c, (r + 1) * cols + c) for r in range(rows - 1) for c in range(cols)]
+    for a, b in vpairs:
+        scopes.append([a, b])
+        values.append([_r6(eps * u()), _r6(eps * u()), _r6(u()), _r6(u())])
+    return {"type": "MARKOV", "cards": [2] * n, "scopes": scopes, "values": values}
+
+
 def potts_grid(rows: int, cols: int, k: int = 4, seed: int = 0) -> dict:
     """R x C k-state Potts grid: unary = exp(U(-1,1)) per state; pairwise =
     e^J on the diagonal, e^-J elsewhere."""

@@ -37,7 +37,8 @@
 extern "C" {
 #endif
 
-#define BNPP_VERSION 201   /* 200: single ops take n_cards (the length of cards); 201: sliced bucket-tree marginals */
+#define BNPP_VERSION 202   /* 200: single ops take n_cards (the length of cards); 201: sliced bucket-tree marginals;
+                              202: single ops return the reference's partition sum (out_sum) */
 
 enum bnpp_status {
     BNPP_OK = 0,
@@ -95,7 +96,19 @@ int bnpp_synchronize(bnpp_ctx *ctx, void *stream);
 int bnpp_out_scope(int n_in, const int *in_ndims, const int *const *in_vars, int elim_var, int cap,
                    int *out_ndims, int *out_vars);
 
-/* --------------------------------------------- single ops (device) */
+/* --------------------------------------------- single ops (device)
+ * out_sum (every single op): NULL, or a DEVICE double that receives, when the
+ * stream reaches it, the reference's running sum of the op (Factor::_partition,
+ * factor.hh:26/47) with its bits: the op's terms added one at a time from 0.0
+ * in fp64 in the reference's loop order -- product / divide / conditioning:
+ * the output entries in linear order of the reference's output scope
+ * (factor.cpp:129-139, 161-172, 226-236); sum_out and a fused bucket: the
+ * INPUT (chain-product) entries in (output entry, summed value) order
+ * (factor.cpp:196-208).  A sequential sum by definition (one wave, ~2e8
+ * terms/s): ask for it only where the caller reads partition().  Single ops
+ * compute the reference's unscaled values, so there is no log10 scale to
+ * return (the VE entry points below carry theirs).  fp32 tables: the fp32
+ * terms, widened, summed in fp64. */
 /* Fused bucket:  out = sum_{elim_var} prod_i in_i   — replaces the bucket body of
  * BN::variable_elimination (model.cpp:414-418):
  *     Factor prod(1.0); for (pf : bucket) prod *= *pf; prod.sum_out(var)
@@ -107,28 +120,28 @@ int bnpp_out_scope(int n_in, const int *in_ndims, const int *const *in_vars, int
  * input makes it a copy (factor.cpp:185-188). */
 int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, int n_in,
                           const void *const *in_tables, const int *in_ndims, const int *const *in_vars,
-                          int elim_var, void *out_table, int out_ndims, const int *out_vars);
+                          int elim_var, void *out_table, int out_ndims, const int *out_vars, double *out_sum);
 
 /* Factor::product (factor.cpp:117-147; factor.hh:35) */
 int bnpp_product(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *a, int a_ndims,
                  const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
-                 const int *out_vars);
+                 const int *out_vars, double *out_sum);
 
 /* Factor::divide (factor.cpp:149-180; factor.hh:36): out = a / b over the
  * union scope (out_vars: any order of it).  The reference asserts on a zero
  * divisor (factor.cpp:165); here it yields inf / nan in that entry. */
 int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *a, int a_ndims,
                 const int *a_vars, const void *b, int b_ndims, const int *b_vars, void *out, int out_ndims,
-                const int *out_vars);
+                const int *out_vars, double *out_sum);
 
 /* Factor::sum_out (factor.cpp:182-212; factor.hh:34) */
 int bnpp_sum_out(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *in, int ndims,
-                 const int *vars, int var, void *out, int out_ndims, const int *out_vars);
+                 const int *vars, int var, void *out, int out_ndims, const int *out_vars, double *out_sum);
 
 /* Factor::conditioning (factor.cpp:214-242; factor.hh:38): out scope = vars minus
  * evidence vars, order preserved (domain.cpp:74-90) */
 int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *cards, const void *in, int ndims,
-                   const int *vars, int n_ev, const int *ev_vars, const int *ev_vals, void *out);
+                   const int *vars, int n_ev, const int *ev_vars, const int *ev_vals, void *out, double *out_sum);
 
 /* ------------------------------------------------------ models (host) */
 typedef struct bnpp_model bnpp_model;
@@ -236,8 +249,9 @@ int bnpp_collective_loopback(void *user, int op, const void *send, void *recv, i
  * 10000, 0.001, model.cpp:749) then FactorGraph::marginal per variable
  * (graph.cpp:393-403).  Evidence is not used, as in the reference.  fp64.
  * out: sum(card) values, var-major; *iterations = update's return value
- * (max_iter when it did not converge).  Factor tables >= 2^31 entries:
- * BNPP_ERR_UNSUPPORTED. */
+ * (max_iter when it did not converge).  Small models run in one workgroup,
+ * larger ones (or any factor table of 2^31+ entries, indexed in 64 bits) as a
+ * multi-workgroup flood (BNPP_BP_MODE=single|multi forces either). */
 int bnpp_sum_product(bnpp_ctx *ctx, const bnpp_model *m, int max_iter, double eps, double *out, int *iterations,
                      double *uptime_ms);
 

@@ -148,6 +148,14 @@ private:
 class MN : public Model {                          // model.hh:106-118
 public:
     MN(std::string name, std::vector<Variable *> &variables, std::vector<Factor *> &factors);
+    // model.cpp:979-999: "MARKOV:", every variable with its neighbours, every factor
+    void write(std::ostream &os) const override;
+    friend std::ostream &operator<<(std::ostream &os, const MN &mn);
+
+private:
+    // the reference's container (model.hh:116), filled in the same order, so
+    // the neighbours print in its iteration order
+    std::unordered_map<const Variable *, std::unordered_set<const Variable *>> _neighbors;
 };
 
 // io.hh:10-19 (return 0 / -1 cannot open / -2 wrong network type)

@@ -417,6 +417,8 @@ CLI_BN = {
 CLI_MN = {
     "mn_grid3x3_pr_mar": (["grid3x3.uai", "grid3x3-PR.uai.evid"], "PR\nMAR\nquit\n"),
     "mn_grid3x3_mar_pr": (["grid3x3.uai", "grid3x3-MAR.uai.evid"], "MAR\npartition\nfoo\nquit\n"),
+    "mn_grid3x3_verbose": (["grid3x3.uai", "grid3x3-PR.uai.evid", "-v"], "PR\nquit\n"),
+    "mn_network_verbose": (["network.uai", "network.uai.evid", "-v"], "quit\n"),
 }
 
 

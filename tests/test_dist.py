@@ -137,3 +137,23 @@ def test_tree_part_assembly(world):
     for rank, marg, _ in res:
         for t in range(64):
             assert marg[t] == pytest.approx(full[t], abs=1e-12), (rank, t)
+
+
+def test_collective_is_cached_per_context():
+    """bnpp.dist.collective_for: one TorchCollective per (context, world) --
+    an nccl one creates its per-lane process groups (and communicators) once,
+    up front, not per call or from inside the engine's launch loop -- with
+    its exchange counters reset for every call."""
+    from bnpp import dist as bdist
+
+    class _Ctx:
+        handle = None
+
+    ctx = _Ctx()
+    a = bdist.collective_for(ctx, None, 4)
+    a.calls, a.bytes_sent = 7, 99
+    b = bdist.collective_for(ctx, None, 4)
+    assert b is a and (b.calls, b.bytes_sent) == (0, 0)
+    assert b.backend == "gloo" and b.pool == [] and b.groups == {}
+    c = bdist.collective_for(ctx, None, 8)
+    assert c is not a and c.world == 8

@@ -356,6 +356,71 @@ def test_split_runs_identical_to_unfused(ctx, capfd, spec):
         assert _close(res[0][1][t], want[t], 1e-5), (t, res[0][1][t], want[t])
 
 
+def _bucket_max_log2(d, rows, cols):
+    """max over x of the product of the column-sweep bucket of each variable
+    above the last row (unary, right pair, down pair), as log2"""
+    vals = {tuple(s): v for s, v in zip(d["scopes"], d["values"])}
+    worst = -1e9
+    for r in range(rows - 1):
+        for c in range(cols):
+            v = r * cols + c
+            un, dn = vals[(v,)], vals[(v, v + cols)]
+            rt = vals[(v, v + 1)] if c + 1 < cols else [1.0] * 4
+            best = max(un[x] * dn[2 * x + y] * rt[2 * x + z] for x in range(2) for y in range(2) for z in range(2))
+            worst = max(worst, math.log2(best))
+    return worst
+
+
+@pytest.mark.parametrize("rows,cols,log2_eps", [(16, 4, 10), (18, 3, 12), (17, 2, 16)])
+def test_split_runs_peaked_potentials(ctx, capfd, rows, cols, log2_eps):
+    """Potentials whose bucket products peak far below 1 (synth.peaked_grid:
+    every bucket above the last row has max <= 2^-log2_eps, so a fused run of
+    F >= 5 buckets carries a rescale 2^-sum(e) with |sum(e)| >= 5 (log2_eps - 1)
+    = 45..95 -- outside the +-32 that round 3's last-table fold covered, where
+    it left the scale unapplied and the values drifted toward underflow).  The
+    rescale is now folded per bucket (chain.cuh chain_fold), so split runs
+    (dense and general addressing, F >= 7), one-thread runs (F <= 6) and one
+    bucket per launch give bit-identical fp32 partitions and tree marginals,
+    and log10 Z agrees with the fp64 oracle (reference arithmetic, factor.cpp:
+    131-143, 199-205; no scaling) to fp32 rounding."""
+    d = synth.peaked_grid(rows, cols, log2_eps=log2_eps, seed=5)
+    assert _bucket_max_log2(d, rows, cols) <= -log2_eps + 1e-9
+    m = bnpp.Model.from_dict(d)
+    col = [i * cols + j for j in range(cols) for i in range(rows)]
+    knobs = [{"BNPP_DEBUG_CHAIN": "1"}, {"BNPP_DEBUG_CHAIN": "1", "BNPP_NO_DENSE": "1"}, {"BNPP_SPLIT_MIN_F": "7"},
+             {"BNPP_NO_SPLIT": "1"}, {"BNPP_NO_SPLIT": "1", "BNPP_CHAIN_RUN_MAX": "6"}, {"BNPP_NO_CHAIN": "1"}]
+    res = []
+    for kn in knobs:
+        os.environ.update(kn)
+        os.environ["BNPP_TREE_SLOTS"] = "3"
+        capfd.readouterr()
+        try:
+            out = [bnpp.partition(ctx, m, {}, "mf", bnpp.F32, order=col)[0],
+                   bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F32, order=col)[0]]
+            res.append(out)
+        finally:
+            for key in list(kn) + ["BNPP_TREE_SLOTS"]:
+                del os.environ[key]
+        if "BNPP_DEBUG_CHAIN" in kn:
+            err = capfd.readouterr().err
+            forms = (5, 6) if "BNPP_NO_DENSE" in kn else (7, 8)
+            assert any("run form %d K=2 F=8" % f in err for f in forms), err[-2000:]
+    for out in res[1:]:
+        assert out == res[0]
+    rz, _ = refcpu.Model.from_dict(d).partition({}, "mf")
+    assert rz > 0.0
+    lz_ref = math.log10(rz)
+    assert abs(res[0][0] - lz_ref) <= 1e-6 * abs(lz_ref), (res[0][0], lz_ref)
+    # fp64: min-fill plan bit-exact vs the oracle, the column sweep to 1e-12
+    lz64, z64, _ = bnpp.partition(ctx, m, {}, "mf", bnpp.F64)
+    assert z64 == rz
+    lz64c = bnpp.partition(ctx, m, {}, "mf", bnpp.F64, order=col)[0]
+    assert abs(lz64c - lz_ref) <= 1e-12 * abs(lz_ref)
+    want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    for t in range(m.n_vars):
+        assert _close(res[0][1][t], want[t], 1e-5), (t, res[0][1][t], want[t])
+
+
 @pytest.mark.parametrize("keep,slow,rows", [(3, 13, 12), (5, 13, 12), (7, 2, 12), (9, 4, 12), (13, 13, 14)])
 def test_tree_chain_kept_sets_match(ctx, keep, slow, rows):
     """Deliveries from kept sets smaller than the separators (the 32x32 path:

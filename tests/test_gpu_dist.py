@@ -3,7 +3,8 @@ the per-rank compute: two ranks (processes) over gloo on the box's GPU, each
 running the engine on its share -- the chain segment of the bucket-tree MAR
 (bnpp_marginals_tree_part), its round-robin targets of the per-target MAR, its
 cutset assignments of the PR -- assembled by one all_reduce / all_gather, and
-compared with the one-rank result.  (On an 8-GPU node the same code runs one
+compared with the one-rank result; on BASELINE config 4 (the Promedas-style
+noisy-OR BN, width 22) also with the reference's own PR and MAR.  (On an 8-GPU node the same code runs one
 rank per GPU over RCCL; bench.py --gpus N.)
 
 Tolerances: the segmented tree associates no differently from the whole tree
@@ -46,8 +47,18 @@ per = bdist.sharded_marginals(a.n_vars, a.cards, rank, world,
                               lambda ts: bnpp.marginals(ctx, a, ev, "mf", bnpp.F64, targets=ts)[0], dist)
 lz = bdist.sharded_partition([0, 35, 17], m.cards, {}, rank, world,
                              lambda e: bnpp.partition(ctx, m, e, "mf", bnpp.F64, order=col)[0], dist)
+# BASELINE config 4 (noisy-OR 50 -> 80, width 22, findings observed): per-target
+# MAR dealt over the ranks, bucket-tree MAR by parts, PR by cutset on diseases
+models = os.path.join(sys.argv[1], "tests", "golden", "models")
+c4 = bnpp.Model.load(os.path.join(models, "noisyor_50_80.uai"))
+ev4 = bnpp.load_evidence(os.path.join(models, "noisyor_50_80.uai.evid"))
+per4 = bdist.sharded_marginals(c4.n_vars, c4.cards, rank, world,
+                               lambda ts: bnpp.marginals(ctx, c4, ev4, "mf", bnpp.F64, targets=ts)[0], dist)
+tree4 = bdist.sharded_tree_marginals(ctx, c4, rank, world, dist, ev4, "mf", bnpp.F64)
+lz4 = bdist.sharded_partition([0, 7, 21], c4.cards, ev4, rank, world,
+                              lambda e: bnpp.partition(ctx, c4, e, "mf", bnpp.F64)[0], dist)
 if rank == 0:
-    print(json.dumps({"tree": tree, "per": per, "lz": lz}))
+    print(json.dumps({"tree": tree, "per": per, "lz": lz, "per4": per4, "tree4": tree4, "lz4": lz4}))
 dist.barrier()
 dist.destroy_process_group()
 ctx.close()
@@ -93,3 +104,20 @@ def test_two_ranks_hip_path_match_one_rank(ctx, tmp_path):
         assert got["per"][str(t)] == p, t
     lz1 = bnpp.partition(ctx, m, {}, "mf", bnpp.F64, order=col)[0]
     assert math.isclose(got["lz"], lz1, rel_tol=1e-12), (got["lz"], lz1)
+
+    # config 4 against the reference's own numbers (config4_golden.json:
+    # BN::partition and the per-target MAR of every disease, model.cpp:250-346)
+    with open(os.path.join(REPO, "tests", "golden", "config4_golden.json")) as f:
+        g = json.load(f)
+    ev4 = bnpp.load_evidence(model_path(g["evidence"]))
+    assert abs(got["lz4"] - g["pr"]["log10Z"]) <= 1e-12 * abs(g["pr"]["log10Z"]), (got["lz4"], g["pr"])
+    for key in ("per4", "tree4"):
+        for t, ref in g["marginals"].items():
+            for x, y in zip(got[key][t], ref["values"]):
+                assert abs(x - y) <= 1e-12, (key, t, got[key][t], ref["values"])
+        for v, x in ev4.items():
+            assert got[key][str(v)] == [1.0 if s == x else 0.0 for s in range(2)], (key, v)
+    c4 = bnpp.Model.load(model_path(g["model"]))
+    per41, _ = bnpp.marginals(ctx, c4, ev4, "mf", bnpp.F64)
+    for t, p in per41.items():
+        assert got["per4"][str(t)] == p, t            # the per-target VEs are the same on any rank

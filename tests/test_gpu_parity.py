@@ -48,8 +48,8 @@ def _cards_list(cards: dict):
     return [cards.get(v, 1) for v in range(n)]
 
 
-def run_bucket(ctx, dtype, cards, inputs, elim, out_vars=None):
-    """inputs: [(scope, values)] -> (out_scope, values list)"""
+def run_bucket(ctx, dtype, cards, inputs, elim, out_vars=None, with_sum=False):
+    """inputs: [(scope, values)] -> (out_scope, values list[, partition sum])"""
     scopes = [s for s, _ in inputs]
     if out_vars is None:
         out_vars = bnpp.out_scope(scopes, elim)
@@ -58,10 +58,22 @@ def run_bucket(ctx, dtype, cards, inputs, elim, out_vars=None):
         size *= cards[v]
     tabs = [_dev(vals, dtype) for _, vals in inputs]
     out = torch.full((size,), float("nan"), dtype=TD[dtype], device=DEV)
+    psum = torch.full((1,), float("nan"), dtype=torch.float64, device=DEV)
     bnpp.bucket_eliminate(ctx, dtype, _cards_list(cards), [t.data_ptr() for t in tabs], scopes, elim,
-                          out.data_ptr(), out_vars, stream=_stream())
+                          out.data_ptr(), out_vars, stream=_stream(), out_sum=psum.data_ptr() if with_sum else None)
     torch.cuda.synchronize()
+    if with_sum:
+        return out_vars, out.cpu().tolist(), psum.item()
     return out_vars, out.cpu().tolist()
+
+
+def _check_sum(dtype, got, want, case):
+    """Factor::_partition: fp64 bit-exact (same terms, same order); fp32 terms
+    summed in fp64: 1e-6 relative"""
+    if dtype == bnpp.F64:
+        assert got == want, (case, got, want)
+    else:
+        assert abs(got - want) <= 1e-6 * abs(want) + 1e-30, (case, got, want)
 
 
 # ------------------------------------------------------------ single ops
@@ -75,16 +87,18 @@ def test_kat_single_ops(ctx, golden_kat, dtype):
     for case in golden_kat["cases"]:
         ref = outs[case["out"]]
         op = case["op"]
+        psum = None
         if op == "product":
             a, b = facs[case["a"]], facs[case["b"]]
-            scope, vals = run_bucket(ctx, dtype, cards, [(a["scope"], a["values"]), (b["scope"], b["values"])], -1)
+            scope, vals, psum = run_bucket(ctx, dtype, cards, [(a["scope"], a["values"]), (b["scope"], b["values"])],
+                                           -1, with_sum=True)
             products[case["out"]] = (scope, ref["values"])     # feed sum_out the reference's exact table
         elif op == "sum_out":
             s, v = products[case["a"]]
-            scope, vals = run_bucket(ctx, dtype, cards, [(s, v)], case["var"])
+            scope, vals, psum = run_bucket(ctx, dtype, cards, [(s, v)], case["var"], with_sum=True)
         elif op == "bucket":
             ins = [(facs[x]["scope"], facs[x]["values"]) for x in case["inputs"]]
-            scope, vals = run_bucket(ctx, dtype, cards, ins, case["var"])
+            scope, vals, psum = run_bucket(ctx, dtype, cards, ins, case["var"], with_sum=True)
         elif op == "cond":
             a = facs[case["a"]]
             ev = {int(k): v for k, v in case["evidence"].items()}
@@ -94,10 +108,11 @@ def test_kat_single_ops(ctx, golden_kat, dtype):
                 size *= cards[v]
             t = _dev(a["values"], dtype)
             out = torch.full((size,), float("nan"), dtype=TD[dtype], device=DEV)
+            ps = torch.full((1,), float("nan"), dtype=torch.float64, device=DEV)
             bnpp.condition(ctx, dtype, _cards_list(cards), t.data_ptr(), a["scope"], ev, out.data_ptr(),
-                           stream=_stream())
+                           stream=_stream(), out_sum=ps.data_ptr())
             torch.cuda.synchronize()
-            vals = out.cpu().tolist()
+            vals, psum = out.cpu().tolist(), ps.item()
         elif op == "divide":              # Factor::divide (factor.cpp:149-180), bnpp_divide
             a, b = facs[case["a"]], facs[case["b"]]
             scope = ref["scope"]
@@ -106,10 +121,11 @@ def test_kat_single_ops(ctx, golden_kat, dtype):
                 size *= cards[v]
             ta, tb = _dev(a["values"], dtype), _dev(b["values"], dtype)
             out = torch.full((size,), float("nan"), dtype=TD[dtype], device=DEV)
+            ps = torch.full((1,), float("nan"), dtype=torch.float64, device=DEV)
             bnpp.divide(ctx, dtype, _cards_list(cards), ta.data_ptr(), a["scope"], tb.data_ptr(), b["scope"],
-                        out.data_ptr(), scope, stream=_stream())
+                        out.data_ptr(), scope, stream=_stream(), out_sum=ps.data_ptr())
             torch.cuda.synchronize()
-            vals = out.cpu().tolist()
+            vals, psum = out.cpu().tolist(), ps.item()
         else:
             continue                      # normalize: host bookkeeping (width <= 1 in MAR)
         assert scope == ref["scope"], case
@@ -118,6 +134,8 @@ def test_kat_single_ops(ctx, golden_kat, dtype):
         else:
             for x, y in zip(vals, ref["values"]):
                 assert abs(x - y) <= 1e-6 * abs(y) + 1e-30, (case, x, y)
+        # Factor::partition() of the op (factor.cpp:139, 172, 208, 236), from the ABI's out_sum
+        _check_sum(dtype, psum, ref["partition"], case)
         checked += 1
     assert checked >= 260
 
@@ -144,7 +162,7 @@ def test_random_buckets_bit_exact_vs_oracle(ctx):
     rng = random.Random(2024)
     for it in range(150):
         cards, ins, elim = _rand_bucket(rng)
-        scope, vals = run_bucket(ctx, bnpp.F64, cards, ins, elim)
+        scope, vals, psum = run_bucket(ctx, bnpp.F64, cards, ins, elim, with_sum=True)
         fs = [refcpu.Factor.new(s, cards, v) for s, v in ins]
         if elim >= 0:
             ref = refcpu.bucket(fs, elim, cards[elim])
@@ -154,6 +172,7 @@ def test_random_buckets_bit_exact_vs_oracle(ctx):
                 ref = ref.product(f)
         assert scope == ref.scope, it
         assert vals == ref.values, it
+        assert psum == ref.partition, (it, psum, ref.partition)
 
 
 @pytest.mark.parametrize("k,n_other", [(2, 12), (4, 6), (2, 9)])
