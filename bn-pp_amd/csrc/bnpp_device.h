@@ -76,7 +76,11 @@ struct BucketDesc {
     int32_t in_span[kMaxDescIn];        // elements of each small input's reachable range
     // chain form (chain != 0): F consecutive buckets of a sweep fused in
     // registers; chain = F | gmask << 8 | form << 16 | dep << 20 (ChainForm, ChainDep)
-    int32_t chain, chain_pad;
+    int32_t chain;
+    // slab form: lanes sharing one output tile (0/1, or 2 when a tile's row is
+    // 32 B: each lane then stores 16 B and a wave's store is one contiguous
+    // 1-KiB run instead of 16-B pieces at a 32-B stride)
+    int32_t lanes;
 };
 
 // arguments of one level launch (a group of buckets of one kernel variant)
@@ -104,7 +108,7 @@ __host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return ni
 // stream kernels: 4096 + big-class * 256 + v1 * 16 + v2  (v1, v2 <= 8)
 __host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 256 + v1 * 16 + v2; }
 // slab kernels (slab.cuh): K summed values, C0 entries of output dim 0, V slow-dim entries per lane
-__host__ __device__ constexpr int slab_key(int k, int c0, int v) { return 16384 + k * 256 + c0 * 16 + v; }
+__host__ __device__ constexpr int slab_key(int k, int c0, int v, int h = 1) { return 16384 + k * 256 + c0 * 16 + v + (h == 2 ? 8 : 0); }
 
 // Chain (sweep) form: F consecutive buckets of an elimination chain in one
 // pass.  Input 0 is the message entering the run; bucket j of the run sums

@@ -52,10 +52,6 @@ namespace {
 thread_local std::string g_err;
 // phase split of this thread's last partition / marginals call (bnpp_last_timing)
 thread_local double g_timing[kTimingPhases] = {0};
-// the context of a one-shot call being planned (create_job with the cached
-// arena): a checkpointed plan, which fills the memory budget, starts mapping
-// its arena there while the checkpoint search goes on
-thread_local Context *g_prefetch_ctx = nullptr;
 
 int set_err(int status, const std::string &msg) {
     g_err = msg;
@@ -313,7 +309,6 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
         } else if (need(plans.back()) > budget || n_parts > 1 || n_slices > 1) {
             // every forward message does not fit: recompute them from checkpoints
             // (chain-shaped trees), with as many checkpoint slots as fit
-            if (need(plans.back()) > budget && g_prefetch_ctx) arena_prefetch(*g_prefetch_ctx, budget);
             std::string msg;
             VEPlan best;
             // sliced runs: the two-front schedule (two concurrent lanes, no
@@ -436,6 +431,48 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
     return BNPP_OK;
 }
 
+// Analysis aid (BNPP_ARENA_PROFILE=path, host only): for every 1-GiB chunk of
+// the arena, the algorithmic bytes the schedule has moved before its first
+// launch touching the chunk -- how early a cold call needs each part of its
+// arena mapped.  One line per chunk: "chunk cum_bytes group".
+void arena_profile(const Schedule &s, int eb, const char *path) {
+    FILE *f = std::fopen(path, "w");
+    if (!f) return;
+    const int64_t G = (int64_t)1 << 30;
+    const int64_t nch = (s.arena_bytes + G - 1) / G;
+    std::vector<double> first(nch, -1);
+    std::vector<int> first_g(nch, -1);
+    double cum = 0;
+    for (size_t gi = 0; gi < s.groups.size(); ++gi) {
+        const Schedule::Group &g = s.groups[gi];
+        double moved = 0;
+        for (int k = g.begin; k < g.end; ++k) {
+            const BucketDesc &d = s.descs[k];
+            int tabs[kMaxDescIn + 1];
+            int nt = 0;
+            for (int i = 0; i < d.n_in && i < kMaxDescIn; ++i) tabs[nt++] = d.in_table[i];
+            tabs[nt++] = d.out_table;
+            for (int i = 0; i < nt; ++i) {
+                const int t = tabs[i];
+                if (t < 0) continue;
+                moved += (double)s.table_size[t] * eb;
+                if (t < (int)s.table_offset.size() && s.table_offset[t] >= 0) {
+                    const int64_t a = s.table_offset[t] / G, b = (s.table_offset[t] + s.table_size[t] * eb - 1) / G;
+                    for (int64_t c = a; c <= b && c < nch; ++c)
+                        if (first[c] < 0) {
+                            first[c] = cum;
+                            first_g[c] = (int)gi;
+                        }
+                }
+            }
+        }
+        cum += moved;
+    }
+    std::fprintf(f, "# arena %lld bytes, %zu groups, %.6g bytes moved\n", (long long)s.arena_bytes, s.groups.size(), cum);
+    for (int64_t c = 0; c < nch; ++c) std::fprintf(f, "%lld %.6g %d\n", (long long)c, first[c], first_g[c]);
+    std::fclose(f);
+}
+
 // Plans -> schedules.  MAR targets are split into batches whose estimated
 // arenas fit `budget` bytes; a batch runs as one level-aligned schedule.
 int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int heuristic, const int *order,
@@ -496,6 +533,7 @@ int plan_schedules(const ModelData &d, const std::vector<int> &ev, int kind, int
         }
         levels += s.n_levels;
         buckets += (double)s.descs.size();
+        if (const char *prof = std::getenv("BNPP_ARENA_PROFILE")) arena_profile(s, eb, prof);
         out.push_back(std::move(s));
     }
     if (timing) std::fprintf(stderr, "[bnpp] schedules %.1f ms total\n", now_ms() - t0);
@@ -573,10 +611,6 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     std::vector<Schedule> batches;
     if (n_parts < 1 || part < 0 || part >= n_parts) return set_err(BNPP_ERR_INVALID, "bad part / n_parts");
     const double tp = now_ms();
-    struct PrefetchScope {
-        explicit PrefetchScope(Context *c) { g_prefetch_ctx = c; }
-        ~PrefetchScope() { g_prefetch_ctx = nullptr; }
-    } prefetch_scope(use_cache ? &ctx->c : nullptr);
     int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype,
                             budget > 0 ? budget : memory_budget(ctx, use_cache), batches, job->stats, part, n_parts,
                             n_slices, slice_rank);

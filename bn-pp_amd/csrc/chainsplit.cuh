@@ -180,26 +180,6 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
     c.left = 0;
 }
 
-#ifndef BNPP_DENSE_JR
-#define BNPP_DENSE_JR 1       // dense runs: G offsets per tile for the boundary bucket only
-#endif
-#ifndef BNPP_SPLIT_FLAT
-#define BNPP_SPLIT_FLAT 0     // 1: one tile per workgroup (flat grid), no prefetch
-#endif
-#ifndef BNPP_SPLIT_FWD_MODE
-#define BNPP_SPLIT_FWD_MODE 0 // single-run forward loop: 0 two register sets alternating, 1 rotation, 2 one tile ahead
-#endif
-#ifndef BNPP_SPLIT_NTL
-#define BNPP_SPLIT_NTL 0      // nontemporal message loads
-#endif
-// timing bisection only (results are wrong with any of these set): drop the
-// running maximum, the per-tile G offsets
-#ifndef BNPP_SPLIT_BISECT
-#define BNPP_SPLIT_BISECT 0   // bit 1 no maximum, bit 2 G offsets 0
-#endif
-#ifndef BNPP_SPLIT_WAVES
-#define BNPP_SPLIT_WAVES 0     // waves per SIMD the register allocation must allow (0: compiler's choice)
-#endif
 // workgroup barrier for the LDS exchange only: waits for this wave's LDS
 // operations, not for its global loads and stores (__syncthreads would wait
 // vmcnt(0) and drain the next tile's prefetched loads)
@@ -213,7 +193,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // per-bucket restaging live in the same body, the uniform state fits the
 // scalar registers (with it: ~80 SGPRs spilled to VGPR lanes, re-read per tile)
 template <int F, int FORM, int DEP, bool DENSE, bool MULTI>
-__global__ __launch_bounds__(64 * (1 << (F - 4))) __attribute__((amdgpu_waves_per_eu(BNPP_SPLIT_WAVES > 0 ? BNPP_SPLIT_WAVES : 1)))
+__global__ __launch_bounds__(64 * (1 << (F - 4)))
 void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const int64_t *__restrict__ pool,
                         TableMeta *__restrict__ meta, int64_t total_vblocks) {
     using T = float;
@@ -294,8 +274,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             // backward) may have a G table varying along rest dim 1 (planner)
             constexpr int JR = FORM == kChainFwd ? F - 1 : 0;
 #pragma unroll
-            for (int j = 0; j < F; ++j)
-                gb[j] = (BNPP_SPLIT_BISECT & 4) == 0 && (j == JR || BNPP_DENSE_JR == 0) ? (int32_t)d1 * c.d_g1[j] : 0;
+            for (int j = 0; j < F; ++j) gb[j] = j == JR ? (int32_t)d1 * c.d_g1[j] : 0;
             return;
         }
         const int64_t tid0 = (vb - cur_begin) * kSplitRows;
@@ -335,10 +314,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             const T *wb = c.big + tin + (int64_t)w * c.d_slab + lane;
             const int64_t step = c.d_slab << (F - 4);
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                if constexpr (BNPP_SPLIT_NTL != 0) rg[e] = __builtin_nontemporal_load((const gbl_t<T> *)(wb + e * step));
-                else rg[e] = gload(wb + e * step);
-            }
+            for (int e = 0; e < 16; ++e) rg[e] = gload(wb + e * step);
         } else if constexpr (DENSE) {
             // 64 input rows of N contiguous values at tin + row * N
             const T *big = c.big + tin;
@@ -346,7 +322,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             for (int it = 0; it < 4; ++it) {
                 const int q = it * 64 + lane;
                 const int rw = w * RPW + q / CPR, ch = q % CPR;
-                const vec_t<T, 4> v = vload<4, kNtLoad || BNPP_SPLIT_NTL != 0, true>(big + (int64_t)rw * N + 4 * ch);
+                const vec_t<T, 4> v = vload<4, kNtLoad, true>(big + (int64_t)rw * N + 4 * ch);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) rg[4 * it + k] = v[k];
             }
@@ -361,9 +337,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
 #pragma unroll
                 for (int p = 0; p < 4; ++p) o += (int64_t)((e >> (3 - p)) & 1) * c.is4[p];
                 const T *sp = wb + o;                      // uniform slab base
-                const T *src = reinterpret_cast<const T *>(reinterpret_cast<const char *>(sp) + lob);
-                if constexpr (BNPP_SPLIT_NTL != 0) rg[e] = __builtin_nontemporal_load((const gbl_t<T> *)src);
-                else rg[e] = gload(src);
+                rg[e] = gload(reinterpret_cast<const T *>(reinterpret_cast<const char *>(sp) + lob));
             }
         } else {
             // 64 input rows of N contiguous values (slot 0 fastest): wave w loads
@@ -374,7 +348,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 const int q = it * 64 + lane;
                 const int rw = w * RPW + q / CPR, ch = q % CPR;
                 const int64_t ro = __shfl(in_off, rw, 64);  // row rw's input offset (held by lane rw)
-                const vec_t<T, 4> v = vload<4, kNtLoad || BNPP_SPLIT_NTL != 0, true>(big + ro + 4 * ch);
+                const vec_t<T, 4> v = vload<4, kNtLoad, true>(big + ro + 4 * ch);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) rg[4 * it + k] = v[k];
             }
@@ -459,7 +433,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         // (no per-tile rescale: it is folded into the G tables, SplitState)
 #pragma unroll
         for (int e = 0; e < 16; ++e)
-            if constexpr ((BNPP_SPLIT_BISECT & 2) == 0) lmax = fmaxf(lmax, t[e]);      // entries are >= 0, never NaN
+            lmax = fmaxf(lmax, t[e]);                                          // entries are >= 0, never NaN
 
         if constexpr (FORM == kChainFwd) {
             // row position of entry e: w * 16 + e (slot 0 most significant)
@@ -517,7 +491,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     float rg[16];
     int64_t in_off, out_off;
     int32_t gb[F];
-    if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0 && (FORM == kChainBwd || BNPP_SPLIT_FWD_MODE == 2)) {
+    if constexpr (!MULTI && FORM == kChainBwd) {
         // one bucket, backward form: the next tile's loads are issued
         // (unconditionally: the last tile is re-read rather than branching, so
         // the wait counts stay static) before the current tile is computed (a
@@ -536,29 +510,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             vb = vbn;
             if (vb >= total_vblocks) break;
         }
-    } else if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0 && BNPP_SPLIT_FWD_MODE == 1) {
-        // forward, two tiles in flight by rotation (t <- A <- B <- new loads)
-        const int64_t last = total_vblocks - 1, g = gridDim.x;
-        auto clamp = [&](int64_t v) { return v < last ? v : last; };
-        float rb[16];
-        decode(vb, in_off, out_off, gb);
-        issue(in_off, rg);
-        decode(clamp(vb + g), in_off, out_off, gb);
-        issue(in_off, rb);
-        while (true) {
-            float t[16];
-#pragma unroll
-            for (int e = 0; e < 16; ++e) t[e] = rg[e];
-#pragma unroll
-            for (int e = 0; e < 16; ++e) rg[e] = rb[e];
-            decode(clamp(vb + 2 * g), in_off, out_off, gb);
-            issue(in_off, rb);
-            decode(vb, in_off, out_off, gb);
-            run_tile(t, out_off, gb);
-            vb += g;
-            if (vb >= total_vblocks) break;
-        }
-    } else if constexpr (!MULTI && BNPP_SPLIT_FLAT == 0) {
+    } else if constexpr (!MULTI) {
         // one bucket, forward form: the loads of the next two tiles are in flight while a
         // tile is computed (register sets A and B alternate: a set is copied
         // out only once its loads are two tiles old, so no wait exposes
@@ -643,7 +595,7 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
         cus = ds.cus[dev];
     }
     const int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
-    const int64_t grid = BNPP_SPLIT_FLAT ? a.vblocks : a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
+    const int64_t grid = a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
     if (a.n_desc == 1)
         hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP, DENSE, false>), dim3((unsigned)grid),
                            dim3(64 * split_waves(F)), shm, stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);

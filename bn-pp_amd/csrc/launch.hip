@@ -3,6 +3,8 @@
 // k_chain_f32/f64).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "bnpp_device.h"
 #include "runtime.hpp"
 
@@ -25,31 +27,37 @@ hipError_t dispatch_slab_single_f64(int key, const SingleArgs &a, hipStream_t st
 hipError_t dispatch_slab_level_f32(int key, const LevelArgs &a, hipStream_t stream);
 hipError_t dispatch_slab_level_f64(int key, const LevelArgs &a, hipStream_t stream);
 
-// Result tables out of the arena, one workgroup per table: 16-B moves while
-// both ends allow them (tables are 256-B aligned in the arena and the results
-// buffer), 4-B ones for the tail (sizes are whole fp32 / fp64 entries).
+// Result tables out of the arena: blockIdx.x picks the table, the
+// kCopyParts workgroups along y share it grid-stride (a multi-GB
+// variable_elimination result would crawl through one workgroup); 16-B moves
+// while both ends allow them (tables are 256-B aligned in the arena and the
+// results buffer), 4-B ones for the tail (sizes are whole fp32 / fp64 entries).
+constexpr int kCopyParts = 64;
 __global__ __launch_bounds__(256) void copy_tables_kernel(const CopyItem *__restrict__ items, int n) {
     const CopyItem c = items[blockIdx.x];
     const int64_t n16 = c.bytes / 16;
+    const int64_t first = (int64_t)blockIdx.y * blockDim.x + threadIdx.x, step = (int64_t)gridDim.y * blockDim.x;
     const uint4 *s16 = static_cast<const uint4 *>(c.src);
     uint4 *d16 = static_cast<uint4 *>(c.dst);
-    for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) d16[i] = s16[i];
+    for (int64_t i = first; i < n16; i += step) d16[i] = s16[i];
     const uint32_t *s4 = static_cast<const uint32_t *>(c.src);
     uint32_t *d4 = static_cast<uint32_t *>(c.dst);
-    for (int64_t i = n16 * 4 + threadIdx.x; i < c.bytes / 4; i += blockDim.x) d4[i] = s4[i];
+    for (int64_t i = n16 * 4 + first; i < c.bytes / 4; i += step) d4[i] = s4[i];
     (void)n;
 }
 
-hipError_t launch_copies(const CopyItem *items, int n, hipStream_t stream) {
+hipError_t launch_copies(const CopyItem *items, int n, int64_t max_bytes, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(copy_tables_kernel, dim3((unsigned)n), dim3(256), 0, stream, items, n);
+    // a workgroup per 64 KiB of the largest table, up to kCopyParts
+    const int64_t parts = std::min<int64_t>(kCopyParts, std::max<int64_t>(1, max_bytes >> 16));
+    hipLaunchKernelGGL(copy_tables_kernel, dim3((unsigned)n, (unsigned)parts), dim3(256), 0, stream, items, n);
     return hipGetLastError();
 }
 
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream) {
     if (a.d.n_tiles <= 0) return hipSuccess;
     if (a.d.big >= 0 && a.d.bcls == kBigSlab) {
-        const int key = slab_key(a.d.k, a.d.v1, a.d.v2);
+        const int key = slab_key(a.d.k, a.d.v1, a.d.v2, a.d.lanes);
         return is_f32 ? dispatch_slab_single_f32(key, a, stream) : dispatch_slab_single_f64(key, a, stream);
     }
     if (a.d.big >= 0) {

@@ -637,6 +637,14 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     if (i != big && sd->s[i] != 0) ok = false;
                 if (ok) {
                     int vn = eb == 4 ? (slab_c0 == 1 ? 4 : slab_c0 == 2 ? 2 : 1) : (slab_c0 == 1 ? 2 : 1);
+                    // A/B knob: slow-dim entries per tile (instantiated: f32 c0=1 {1,4}, 2 {1,2},
+                    // 4 {1,2}; f64 c0=1 {1,2}, 2 {1,2}, 4 {1}; slab.cuh)
+                    if (const char *sv = std::getenv("BNPP_SLAB_V")) {
+                        const int want = std::atoi(sv);
+                        const bool inst = want == 1 || (want == 2 && slab_c0 != 1 && (eb == 4 || slab_c0 == 2)) ||
+                                          (want == 2 && eb == 8 && slab_c0 == 1) || (want == 4 && eb == 4 && slab_c0 == 1);
+                        if (inst) vn = want;
+                    }
                     if ((int64_t)sd->card % vn || b.in[big].base % vn || es[big] % vn) vn = 1;
                     slab_v = vn;
                 }
@@ -649,6 +657,9 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 d.n_tiles = out_size / (v1 * v2);
                 d.big = big;
                 d.bcls = kBigSlab;
+                // 32-B rows (f64 c0 * v = 4, f32 8): two lanes per tile, 16 B each
+                const char *sl = std::getenv("BNPP_SLAB_LANES");     // A/B knob: 1 = one lane per tile
+                d.lanes = v1 * v2 * eb == 32 && !(sl && *sl == '1') ? 2 : 1;
                 for (int i = 0; i < n; ++i) {
                     d.in_span[i] = (int32_t)std::min<int64_t>(span[i], INT32_MAX);
                     d.in_lds_off[i] = 0;
@@ -2312,7 +2323,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
         it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf)
-                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2)
+                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes)
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2)
                  : b.simple ? variant_key(kMaxIn, 1, 1)         // the widest input class runs any input count
                             : variant_key(it.d.n_in, it.d.v1, it.d.v2);
@@ -2354,7 +2365,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
             const Item &it = items[ord[i]];
             BucketDesc &d = s.descs[i];
             d.vblk_begin = vb;
-            const int64_t per_vb = d.chain && chain_split_form((d.chain >> 16) & 0xf) ? kSplitRowsHost : kBlock;
+            const int64_t per_vb = d.chain && chain_split_form((d.chain >> 16) & 0xf) ? kSplitRowsHost
+                                   : d.big >= 0 && d.bcls == kBigSlab && d.lanes == 2 ? kBlock / 2 : kBlock;
             vb += (d.n_tiles + per_vb - 1) / per_vb;
             g.small_elems = std::max(g.small_elems, d.big >= 0 || d.chain ? d.small_elems : 0);
             if (dump && d.chain) {

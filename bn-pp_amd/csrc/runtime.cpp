@@ -327,37 +327,7 @@ void free_executable(Context &ctx, Executable &ex) {
     ex = Executable{};
 }
 
-void arena_prefetch(Context &ctx, int64_t bytes) {
-    if (ctx.prefetch.joinable() || bytes <= 0) return;
-    if (ctx.arena_cache && (double)ctx.arena_cache_bytes >= 0.95 * (double)bytes) return;
-    ctx.prefetch_ptr = nullptr;
-    ctx.prefetch_bytes = bytes;
-    const int dev = ctx.device;
-    void **slot = &ctx.prefetch_ptr;
-    ctx.prefetch = std::thread([dev, bytes, slot]() {
-        void *p = nullptr;
-        if (hipSetDevice(dev) == hipSuccess && hipMalloc(&p, (size_t)bytes) != hipSuccess) p = nullptr;
-        *slot = p;
-    });
-}
-
-void arena_prefetch_join(Context &ctx) {
-    if (!ctx.prefetch.joinable()) return;
-    ctx.prefetch.join();
-    void *p = ctx.prefetch_ptr;
-    ctx.prefetch_ptr = nullptr;
-    if (!p) return;                                    // mapping failed: make_program allocates as before
-    if (ctx.arena_cache && ctx.arena_cache_bytes >= ctx.prefetch_bytes) {
-        (void)hipFree(p);
-        return;
-    }
-    if (ctx.arena_cache) (void)hipFree(ctx.arena_cache);
-    ctx.arena_cache = p;
-    ctx.arena_cache_bytes = ctx.prefetch_bytes;
-}
-
 void drop_arena_cache(Context &ctx) {
-    arena_prefetch_join(ctx);
     if (ctx.arena_cache) (void)hipFree(ctx.arena_cache);
     ctx.arena_cache = nullptr;
     ctx.arena_cache_bytes = 0;
@@ -372,19 +342,17 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
     hipError_t err = hipSetDevice(ctx.device);
     if (err != hipSuccess) return fail(ctx, err, "hipSetDevice");
     const int64_t need = std::max<int64_t>(pg.arena_bytes, 256);
-    bool prefetched = false;
-    if (use_cache && ctx.prefetch.joinable()) {
-        const auto tj = std::chrono::steady_clock::now();
-        arena_prefetch_join(ctx);                      // the part of the mapping planning did not hide
-        pg.arena_alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tj).count();
-        prefetched = true;
-    }
     if (use_cache && ctx.arena_cache && ctx.arena_cache_bytes >= need) {
         pg.arena = ctx.arena_cache;
         pg.arena_cached = true;
-        pg.arena_reused = !prefetched;
+        pg.arena_reused = true;
     } else {
         if (use_cache) drop_arena_cache(ctx);            // too small: replace it
+        // the plan's own size (not the budget).  This hipMalloc is where a
+        // cold call waits for the driver to clear HBM another process (or
+        // this one) freed shortly before -- ~36 GB/s of backlog, one wait
+        // whatever the size asked (tools/map_probe.hip,
+        // profiles/r04_map_probe.log) -- so it is timed on its own
         const auto ta = std::chrono::steady_clock::now();
         if ((err = hipMalloc(&pg.arena, (size_t)need)) != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
         pg.arena_alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
@@ -426,6 +394,7 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
                           ex.sched.table_size[t] * eb});
         }
         ex.n_copies = (int)cp.size();
+        for (const CopyItem &c : cp) ex.copy_max_bytes = std::max(ex.copy_max_bytes, c.bytes);
         if (!cp.empty()) {
             void *pc = nullptr;
             if ((err = get_buffer(ctx, sizeof(CopyItem) * cp.size(), &pc, &ex.cap_copies)) != hipSuccess)
@@ -447,7 +416,7 @@ int launch_program(Context &ctx, Program &pg, hipStream_t stream) {
         int rc = launch(ctx, ex, stream, &pg.hooks);
         if (rc) return rc;
         if (ex.n_copies > 0) {
-            hipError_t err = launch_copies(ex.d_copies, ex.n_copies, stream);
+            hipError_t err = launch_copies(ex.d_copies, ex.n_copies, ex.copy_max_bytes, stream);
             if (err != hipSuccess) return fail(ctx, err, "launch_copies");
         }
     }

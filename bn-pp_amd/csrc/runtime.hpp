@@ -78,12 +78,6 @@ struct Context {
     // allocator the context holds on to it until it is destroyed
     void *arena_cache = nullptr;
     int64_t arena_cache_bytes = 0;
-    // an arena being mapped on a helper thread while the host still plans
-    // (arena_prefetch): a cold call's hipMalloc of a few hundred GB costs
-    // 0.1-0.3 s, which then overlaps the checkpoint search
-    std::thread prefetch;
-    void *prefetch_ptr = nullptr;
-    int64_t prefetch_bytes = 0;
     // small device buffers (sources, descriptors, dims pool, metadata, results)
     // kept for reuse: a one-shot call otherwise pays ~10 hipMalloc / hipFree
     // pairs (hipFree synchronises), several ms of a small model's PR
@@ -130,6 +124,7 @@ struct Executable {
     std::vector<TableMeta> h_meta;
     CopyItem *d_copies = nullptr;       // result tables -> the program's results buffer
     int n_copies = 0;
+    int64_t copy_max_bytes = 0;         // the largest of them
     // lanes: events a group records (-1: none) and the events it waits for
     // (producers of its inputs on the other lane); events[0] starts lane 1
     // after the metadata reset, events[1] joins it back before the results
@@ -149,7 +144,7 @@ struct Program {
     int64_t arena_bytes = 0;
     bool arena_cached = false;          // arena is the context's cache (not freed with the program)
     bool arena_reused = false;          // ... and was already allocated before this program
-    double arena_alloc_ms = 0;          // hipMalloc of the arena (0 when reused)
+    double arena_alloc_ms = 0;          // hipMalloc of the arena (0 when reused), incl. the driver's HBM clearing wait
     void *results = nullptr;
     size_t results_cap = 0;
     int64_t results_bytes = 0;
@@ -170,13 +165,9 @@ void free_executable(Context &ctx, Executable &ex);
 int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg,
                  bool use_cache = false);
 // copy n result tables (device array of CopyItem) in one launch (launch.hip)
-hipError_t launch_copies(const CopyItem *items, int n, hipStream_t stream);
+hipError_t launch_copies(const CopyItem *items, int n, int64_t max_bytes, hipStream_t stream);
 // release the context's cached arena
 void drop_arena_cache(Context &ctx);
-// start mapping an arena of `bytes` on a helper thread unless the cached one
-// is about that big already; arena_prefetch_join makes it the cached arena
-void arena_prefetch(Context &ctx, int64_t bytes);
-void arena_prefetch_join(Context &ctx);
 int launch_program(Context &ctx, Program &pg, hipStream_t stream);
 // result values (as stored, double) and exp2 of every plan, batches in order
 int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std::vector<double>> &vals,

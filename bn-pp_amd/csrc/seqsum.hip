@@ -51,7 +51,6 @@ __global__ __launch_bounds__(64) void seq_sum_kernel(SeqSumArgs a) {
         }
         // the 64 terms in order, one add at a time (uniform)
         const int64_t left = a.n_terms - base;
-#pragma unroll
         for (int j = 0; j < 64; ++j) {
             if (j >= left) break;
             s = s + __shfl(t, j, 64);

@@ -102,7 +102,24 @@ __device__ __forceinline__ void slab_load_big(const T *bp, int64_t es, T (&m)[K]
     for (int v = 0; v < K; ++v) load_n<T, V, NTL, true>(bp + (int64_t)v * es, m[v]);
 }
 
-template <typename T, int K, int C0, int V>
+// H lanes share one tile (H = 2 for 32-B tile rows): both load the tile's K * V
+// big entries (the same addresses: one transaction) and compute it whole; lane
+// h stores entries [h * N/H, (h+1) * N/H), so a wave's store instruction writes
+// one contiguous run (a 32-B row per lane would write 16-B pieces at a 32-B
+// stride per instruction: 0.68 of HBM peak for the f64 bench bucket)
+template <typename T, int N, int H, bool NT>
+__device__ __forceinline__ void slab_store(T *row, const T (&acc)[N], int h) {
+    if constexpr (H == 1) {
+        store_n<T, N, NT, true>(row, acc);
+    } else {
+        T part[N / H];
+#pragma unroll
+        for (int e = 0; e < N / H; ++e) part[e] = h ? acc[N / H + e] : acc[e];
+        store_n<T, N / H, NT, true>(row + h * (N / H), part);
+    }
+}
+
+template <typename T, int K, int C0, int V, int H>
 __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs args) {
 #if defined(__HIP_DEVICE_COMPILE__)
     (void)args;
@@ -112,7 +129,8 @@ __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs ar
 #endif
     using ST = SlabTile<T, K, C0, V>;
     const BucketDesc &d = a.d;
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t t = H == 1 ? gt : gt / H;
     if (t >= d.n_tiles) return;
     const int big = d.big;
     T m[K][V];
@@ -121,13 +139,13 @@ __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs ar
     ST::compute(m, big, d.n_in, [&](int i, T (&g)[K][C0]) {
         ST::load_small(static_cast<const T *>(a.meta[i].ptr) + d.in_base[i], d.elim_stride[i], slab_sy(d, a.pool, i), g);
     }, acc);
-    store_n<T, ST::N, true, true>(static_cast<T *>(a.meta[d.n_in].ptr) + t * ST::N, acc);
+    slab_store<T, ST::N, H, true>(static_cast<T *>(a.meta[d.n_in].ptr) + t * ST::N, acc, (int)(gt & (H - 1)));
 }
 
 // Level form: one workgroup per virtual block of a level's slab buckets (flat
 // grid), with the VE rescaling (kScale) and the max tracking (kTrackMax) of
 // the other level kernels.
-template <typename T, int K, int C0, int V>
+template <typename T, int K, int C0, int V, int H>
 __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                             const int64_t *__restrict__ pool,
                                                             TableMeta *__restrict__ meta) {
@@ -138,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
     const BucketDesc &d = descs[bi];
     const int64_t *dims = pool + d.dim_off;
     const int big = d.big;
-    const int64_t t = (vb - d.vblk_begin) * kBlock + threadIdx.x;
+    const int64_t t = (vb - d.vblk_begin) * (kBlock / H) + threadIdx.x / H;     // H lanes per tile
     const bool live = t < d.n_tiles;
     T m[K][V];
     if (live)
@@ -171,7 +189,8 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
         }
 #pragma unroll
         for (int e = 0; e < ST::N; ++e) lmax = acc[e] > lmax ? acc[e] : lmax;
-        store_n<T, ST::N, kNtStore, true>(static_cast<T *>(meta[d.out_table].ptr) + t * ST::N, acc);
+        slab_store<T, ST::N, H, kNtStore>(static_cast<T *>(meta[d.out_table].ptr) + t * ST::N, acc,
+                                           (int)(threadIdx.x & (H - 1)));
     }
     if (d.flags & kTrackMax) {
         // one atomic per workgroup at most, skipped when the table's max
@@ -192,30 +211,32 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
     }
 }
 
-template <typename T, int K, int C0, int V>
+template <typename T, int K, int C0, int V, int H>
 static hipError_t go_slab_single(const SingleArgs &a, hipStream_t stream) {
-    const int64_t blocks = (a.d.n_tiles + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((slab_single_kernel<T, K, C0, V>), dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
+    const int64_t blocks = (a.d.n_tiles * H + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((slab_single_kernel<T, K, C0, V, H>), dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
     return hipGetLastError();
 }
 
-template <typename T, int K, int C0, int V>
+template <typename T, int K, int C0, int V, int H>
 static hipError_t go_slab_level(const LevelArgs &a, hipStream_t stream) {
-    hipLaunchKernelGGL((slab_level_kernel<T, K, C0, V>), dim3((unsigned)a.vblocks), dim3(kBlock), 0, stream, a.descs,
+    hipLaunchKernelGGL((slab_level_kernel<T, K, C0, V, H>), dim3((unsigned)a.vblocks), dim3(kBlock), 0, stream, a.descs,
                        a.n_desc, a.pool, a.meta);
     return hipGetLastError();
 }
 
-// instantiated shapes: K = 1..4 summed values; (C0, V): f32 (1,1) (1,4) (2,1)
-// (2,2) (4,1); f64 (1,1) (1,2) (2,1) (4,1)
-#define BNPP_SLAB_K(X, T, C0, V) X(T, 1, C0, V) X(T, 2, C0, V) X(T, 3, C0, V) X(T, 4, C0, V)
-#define BNPP_SLAB_F32(X, T) BNPP_SLAB_K(X, T, 1, 1) BNPP_SLAB_K(X, T, 1, 4) BNPP_SLAB_K(X, T, 2, 1) \
-    BNPP_SLAB_K(X, T, 2, 2) BNPP_SLAB_K(X, T, 4, 1)
-#define BNPP_SLAB_F64(X, T) BNPP_SLAB_K(X, T, 1, 1) BNPP_SLAB_K(X, T, 1, 2) BNPP_SLAB_K(X, T, 2, 1) \
-    BNPP_SLAB_K(X, T, 4, 1)
-#define BNPP_CASE_SLAB_SINGLE(T, K, C0, V) \
-    case slab_key(K, C0, V): return go_slab_single<T, K, C0, V>(a, stream);
-#define BNPP_CASE_SLAB_LEVEL(T, K, C0, V) \
-    case slab_key(K, C0, V): return go_slab_level<T, K, C0, V>(a, stream);
+// instantiated shapes: K = 1..4 summed values; (C0, V, H): f32 (1,1) (1,4)
+// (2,1) (2,2) (4,1) (4,2) and (4,2,2); f64 (1,1) (1,2) (2,1) (4,1) (2,2) and
+// the 32-B rows again as (2,2,2) (4,1,2) -- H = 2 where a tile row is 32 B
+// (planner; BNPP_SLAB_LANES=1 keeps H = 1 for A/B)
+#define BNPP_SLAB_K(X, T, C0, V, H) X(T, 1, C0, V, H) X(T, 2, C0, V, H) X(T, 3, C0, V, H) X(T, 4, C0, V, H)
+#define BNPP_SLAB_F32(X, T) BNPP_SLAB_K(X, T, 1, 1, 1) BNPP_SLAB_K(X, T, 1, 4, 1) BNPP_SLAB_K(X, T, 2, 1, 1) \
+    BNPP_SLAB_K(X, T, 2, 2, 1) BNPP_SLAB_K(X, T, 4, 1, 1) BNPP_SLAB_K(X, T, 4, 2, 1) BNPP_SLAB_K(X, T, 4, 2, 2)
+#define BNPP_SLAB_F64(X, T) BNPP_SLAB_K(X, T, 1, 1, 1) BNPP_SLAB_K(X, T, 1, 2, 1) BNPP_SLAB_K(X, T, 2, 1, 1) \
+    BNPP_SLAB_K(X, T, 4, 1, 1) BNPP_SLAB_K(X, T, 2, 2, 1) BNPP_SLAB_K(X, T, 2, 2, 2) BNPP_SLAB_K(X, T, 4, 1, 2)
+#define BNPP_CASE_SLAB_SINGLE(T, K, C0, V, H) \
+    case slab_key(K, C0, V, H): return go_slab_single<T, K, C0, V, H>(a, stream);
+#define BNPP_CASE_SLAB_LEVEL(T, K, C0, V, H) \
+    case slab_key(K, C0, V, H): return go_slab_level<T, K, C0, V, H>(a, stream);
 
 }  // namespace bnpp

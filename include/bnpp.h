@@ -69,7 +69,9 @@ static inline int bnpp_abi_matches(void) { return bnpp_version() == BNPP_VERSION
  *   out[2] device program (arena, descriptors)     out[3] launch enqueue
  *   out[4] device run + result fetch                out[5] free
  *   out[6] total                                    out[7] 1 if the context's cached arena was reused
- *   out[8] of out[2]: the arena's hipMalloc (0 when reused)
+ *   out[8] of out[2]: the arena's hipMalloc (0 when reused) -- where a call
+ *          waits for the driver to clear HBM that was freed shortly before
+ *          (by any process: ~36 GB/s of backlog on MI355X)
  * Writes min(n, 9) values. */
 int bnpp_last_timing(double *out, int n);
 

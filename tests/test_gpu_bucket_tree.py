@@ -371,7 +371,7 @@ def _bucket_max_log2(d, rows, cols):
     return worst
 
 
-@pytest.mark.parametrize("rows,cols,log2_eps", [(16, 4, 10), (18, 3, 12), (17, 2, 16)])
+@pytest.mark.parametrize("rows,cols,log2_eps", [(16, 4, 10), (18, 3, 12), (17, 3, 13)])
 def test_split_runs_peaked_potentials(ctx, capfd, rows, cols, log2_eps):
     """Potentials whose bucket products peak far below 1 (synth.peaked_grid:
     every bucket above the last row has max <= 2^-log2_eps, so a fused run of
