@@ -269,7 +269,13 @@ def fp64_bucket(ctx, dev, stream, rank, k=4, w=14, steps=10):
         for x in range(k):
             acc = acc + M[x, s_i] * F[x, y_i]
     torch.cuda.synchronize(dev)
-    return {"workload": "potts-k%d bucket m(x,S_1..S_%d)*f(x,y)->sum_x, f64" % (k, w),
+    traffic = None
+    for tpath in sorted(glob.glob(os.path.join(REPO, "profiles", "traffic_r*.json")), reverse=True):
+        tj = json.load(open(tpath))
+        if tj.get("k") == k and tj.get("w") == w and tj.get("dtype") == "f64":
+            traffic = tj.get("hbm_bytes_per_launch")
+            break
+    return {"workload": "potts-k%d bucket m(x,S_1..S_%d)*f(x,y)->sum_x, f64" % (k, w), "traffic": traffic,
             "factor_entries_per_s": float(k ** (w + 2)) / (kern_ms * 1e-3), "kernel_ms": kern_ms,
             "alg_bytes_per_launch": alg, "achieved_GBps": alg / (kern_ms * 1e-3) / 1e9,
             "frac": alg / (kern_ms * 1e-3) / HBM_PEAK, "spot_check_exact": bool(torch.equal(out[idx], acc))}

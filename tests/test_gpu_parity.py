@@ -542,3 +542,22 @@ def test_partition_corpus_matches_reference(ctx):
         m = bnpp.Model.load(model_path(c["model"]))
         lz, _, _ = bnpp.partition(ctx, m, evidence_of(c["evidence"]), "mf", bnpp.F64)
         assert abs(lz - c["log10Z"]) <= 1e-9, (c["model"], c["evidence"], lz, c["log10Z"])
+
+
+def test_source_cache_never_serves_another_model(ctx):
+    """The context keeps uploaded sources per model (capi.cpp cached_sources):
+    repeated calls reuse them, and a model with the same shape but other
+    values -- created after the first is freed, possibly at the same address
+    -- gets its own (model uids are never reused)."""
+    from bnpp import synth
+    outs = []
+    for seed in (1, 2, 1):
+        d = synth.ising_grid(5, 6, seed=seed)
+        m = bnpp.Model.from_dict(d)
+        z1 = bnpp.partition(ctx, m, {}, "mf", bnpp.F64)[1]
+        z2 = bnpp.partition(ctx, m, {}, "mf", bnpp.F64)[1]
+        rz, _ = refcpu.Model.from_dict(d).partition({}, "mf")
+        assert z1 == z2 == rz, (seed, z1, z2, rz)
+        outs.append(z1)
+        del m
+    assert outs[0] == outs[2] and outs[0] != outs[1]

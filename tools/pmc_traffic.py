@@ -24,14 +24,16 @@ def main():
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--w", type=int, default=14)
     ap.add_argument("--kernel", default="slab_single_kernel")
+    ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
     args = ap.parse_args()
     f, nf = per_launch(args.fetch, "FETCH_SIZE", args.kernel)
     w, nw = per_launch(args.write, "WRITE_SIZE", args.kernel)
     names = {r["Kernel_Name"] for r in csv.DictReader(open(args.fetch)) if args.kernel in r["Kernel_Name"]}
     S = args.k ** args.w
-    alg = 4 * (args.k * S + args.k * args.k + S * args.k)
+    eb = 4 if args.dtype == "f32" else 8
+    alg = eb * (args.k * S + args.k * args.k + S * args.k)
     print(json.dumps({
-        "k": args.k, "w": args.w, "dtype": "f32", "kernel": sorted(names),
+        "k": args.k, "w": args.w, "dtype": args.dtype, "kernel": sorted(names),
         "launches": [nf, nw],
         "FETCH_SIZE_KB_per_launch": f, "WRITE_SIZE_KB_per_launch": w,
         "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
