@@ -494,8 +494,9 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     if constexpr (!MULTI && FORM == kChainBwd) {
         // one bucket, backward form: the next tile's loads are issued
         // (unconditionally: the last tile is re-read rather than branching, so
-        // the wait counts stay static) before the current tile is computed (a
-        // second tile in flight measured no faster here)
+        // the wait counts stay static) before the current tile is computed (two
+        // tiles ahead, as the forward form: 6.37-6.42 against 6.33-6.41 ms per
+        // 2^32-entry message, profiles/r04_split_ab.txt)
         decode(vb, in_off, out_off, gb);
         issue(in_off, rg);
         while (true) {
