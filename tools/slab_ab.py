@@ -32,12 +32,8 @@ def main():
         f_t = torch.rand(k * k, generator=g, device=dev, dtype=tdt) + 0.5
         outs = {}
         for r in range(rounds):
-            for v in ("1", "1l", "2", "2l"):
-                os.environ["BNPP_SLAB_V"] = v[0]
-                if v.endswith("l"):
-                    os.environ["BNPP_SLAB_LANES"] = "1"
-                else:
-                    os.environ.pop("BNPP_SLAB_LANES", None)
+            for v in ("1:2", "1:1", "2:2", "2:1"):
+                os.environ["BNPP_SLAB_V"], os.environ["BNPP_SLAB_LANES"] = v.split(":")
                 out = torch.empty(S * k, device=dev, dtype=tdt)
 
                 def step():
@@ -59,7 +55,7 @@ def main():
                     assert torch.equal(outs[v], out)
                 outs[v] = out
         for v in outs:
-            assert torch.equal(outs["1"], outs[v])            # same bits whatever the tile shape
+            assert torch.equal(outs["1:2"], outs[v])          # same bits whatever the tile shape
         del m_t, f_t, outs
         torch.cuda.empty_cache()
     os.environ.pop("BNPP_SLAB_V", None)
@@ -67,7 +63,8 @@ def main():
     for (d, v), ms in sorted(res.items()):
         eb = 4 if d == "f32" else 8
         alg = eb * (2 * k * S + k * k)
-        print(json.dumps({"dtype": d, "slab_v": int(v[0]), "lanes_per_32B_row": 1 if v.endswith("l") else 2, "kernel_ms": ms, "GBps": alg / ms / 1e6,
+        print(json.dumps({"dtype": d, "slab_v": int(v[0]), "lanes_per_32B_row": int(v[2]),
+                          "kernel_ms": ms, "GBps": alg / ms / 1e6,
                           "frac": alg / ms / 1e6 / 8000.0}), flush=True)
     ctx.close()
 
