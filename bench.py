@@ -143,7 +143,12 @@ def mar_wallclock(ctx, rank, world, dist, dev, rows, cols, dtype_name, column_or
     name = "ising%dx%d" % (rows, cols)
     rec = {"instance": "%s all marginals, bucket tree, %s order, %s" % (
                name, "column-sweep (width %d)" % rows if column_order else "min-fill", dtype_name),
-           "wall_ms": ms, "cold_wall_ms": cold_ms, "n_gpus": world, "p_var0": marg[0],
+           "wall_ms": ms, "cold_wall_ms": cold_ms,
+           # the cold call's arena hipMalloc, where it waits for the driver to
+           # clear HBM freed before it (by any process; DESIGN §7 "Cold calls")
+           "cold_arena_alloc_ms": cold_phases.get("arena_alloc_ms"),
+           "cold_wall_ms_excl_arena_alloc": cold_ms - (cold_phases.get("arena_alloc_ms") or 0.0),
+           "n_gpus": world, "p_var0": marg[0],
            "phases_ms": {"cold": cold_phases, "warm": warm_phases},
            "max_sum_err": max(abs(sum(p) - 1.0) for p in marg.values())}
     if rank == 0:
