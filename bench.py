@@ -270,9 +270,12 @@ def fp64_bucket(ctx, dev, stream, rank, k=4, w=14, steps=10):
     s_i, y_i = idx // k, idx % k
     M, F = m_t.reshape(k, S), f_t.reshape(k, k)
     acc = torch.zeros(512, device=dev, dtype=torch.float64)
-    with torch.cuda.stream(stream):
-        for x in range(k):
-            acc = acc + M[x, s_i] * F[x, y_i]
+    # on the default stream, like idx above (the bucket's stream is idle after
+    # the synchronize); indexing on `stream` with indices made on the default
+    # stream raced them -- garbage indices, a faulting gather (two ranks on
+    # one GPU, round 4)
+    for x in range(k):
+        acc = acc + M[x, s_i] * F[x, y_i]
     torch.cuda.synchronize(dev)
     traffic = None
     for tpath in sorted(glob.glob(os.path.join(REPO, "profiles", "traffic_r*.json")), reverse=True):

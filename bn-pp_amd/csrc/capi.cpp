@@ -18,6 +18,7 @@
 #include <string>
 #include <utility>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "model_io.hpp"
@@ -43,6 +44,13 @@ struct bnpp_ctx {
     };
     std::mutex src_mu;
     std::vector<Src> srcs;
+    // the last one-shot partition / marginals job (plan, schedule, device
+    // program on the cached arena), relaunched as is by an identical call
+    // (same model, evidence, order, targets, dtype, part, memory budget and
+    // BNPP_* environment): a serving caller's repeated query skips ordering
+    // and planning.  Guarded by cache_mu, like the arena it runs in
+    bnpp_job *job_cached = nullptr;
+    uint64_t job_key = 0;
 };
 struct bnpp_model {
     ModelData d;
@@ -633,6 +641,8 @@ int cached_sources(bnpp_ctx *ctx, const bnpp_model *m, int dtype, std::shared_pt
     return BNPP_OK;
 }
 
+void evict_cached_job(bnpp_ctx *ctx);
+
 int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals,
                int heuristic, const int *order, int n_order, int n_targets, const int *targets, int dtype,
                std::unique_ptr<bnpp_job> &job, int part = 0, int n_parts = 1, bool use_cache = false, int n_slices = 1,
@@ -660,6 +670,7 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     }
     std::vector<Schedule> batches;
     if (n_parts < 1 || part < 0 || part >= n_parts) return set_err(BNPP_ERR_INVALID, "bad part / n_parts");
+    if (use_cache) evict_cached_job(ctx);          // it runs in the arena this job may replace
     const double tp = now_ms();
     int rc = plan_schedules(d, job->ev_val, kind, heuristic, order, n_order, job->targets, dtype,
                             budget > 0 ? budget : memory_budget(ctx, use_cache), batches, job->stats, part, n_parts,
@@ -692,6 +703,42 @@ void destroy_job(bnpp_job *job) {
     free_program(job->ctx->c, job->pg);
     job->src.reset();                               // the context's source cache may keep it
     delete job;
+}
+
+void evict_cached_job(bnpp_ctx *ctx) {
+    if (ctx && ctx->job_cached) {
+        destroy_job(ctx->job_cached);
+        ctx->job_cached = nullptr;
+        ctx->job_key = 0;
+    }
+}
+
+// key of a one-shot call for the job cache (0: do not cache)
+uint64_t call_key(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
+                  const int *order, int n_order, int n_targets, const int *targets, int dtype, int part, int n_parts,
+                  int64_t budget) {
+    if (std::getenv("BNPP_NO_JOB_CACHE")) return 0;
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+    mix(m->uid);
+    mix((uint64_t)kind);
+    std::vector<int> ev(m->d.cards.size(), -1);            // evidence as a per-variable array
+    for (int i = 0; i < n_ev; ++i)
+        if (ev_vars && ev_vals && ev_vars[i] >= 0 && ev_vars[i] < (int)ev.size()) ev[ev_vars[i]] = ev_vals[i];
+    for (int x : ev) mix((uint32_t)x);
+    mix((uint64_t)heuristic);
+    mix((uint64_t)n_order);
+    for (int i = 0; i < n_order && order; ++i) mix((uint32_t)order[i]);
+    mix((uint64_t)(targets ? n_targets : -1));
+    for (int i = 0; i < n_targets && targets; ++i) mix((uint32_t)targets[i]);
+    mix((uint64_t)dtype);
+    mix((uint64_t)part);
+    mix((uint64_t)n_parts);
+    mix((uint64_t)(budget >> 30));                       // the plan depends on the budget (GiB)
+    for (char **e = environ; e && *e; ++e)               // planner / kernel knobs
+        if (std::strncmp(*e, "BNPP_", 5) == 0)
+            for (const char *c = *e; *c; ++c) mix((unsigned char)*c);
+    return h ? h : 1;
 }
 
 // results of a launched job: partition -> out[0] = log10 Z (z_out: Z);
@@ -783,6 +830,39 @@ int job_results_sliced(bnpp_job *job, hipStream_t stream, double *out, int64_t *
     return BNPP_OK;
 }
 
+// A one-shot call's job: the context's cached one when the call is identical
+// (its planning phases read 0), else a new one (create).  cache_ok: the call
+// holds cache_mu (it runs in the cached arena)
+template <typename Create>
+int oneshot_job(bnpp_ctx *ctx, bool cache_ok, uint64_t key, Create &&create, bnpp_job *&job) {
+    job = nullptr;
+    if (cache_ok && key && ctx->job_cached && ctx->job_key == key) {
+        job = ctx->job_cached;
+        ctx->job_cached = nullptr;
+        ctx->job_key = 0;
+        for (int i = 0; i < 3; ++i) g_timing[i] = 0;
+        g_timing[7] = 1;
+        g_timing[8] = 0;
+        return BNPP_OK;
+    }
+    std::unique_ptr<bnpp_job> j;
+    const int rc = create(j);
+    job = j.release();
+    return rc;
+}
+
+// after the call: keep a good job for the next identical call, free the rest
+void oneshot_done(bnpp_ctx *ctx, bool cache_ok, uint64_t key, bnpp_job *job, int rc) {
+    if (!job) return;
+    if (rc == BNPP_OK && cache_ok && key) {
+        evict_cached_job(ctx);
+        ctx->job_cached = job;
+        ctx->job_key = key;
+    } else {
+        destroy_job(job);
+    }
+}
+
 // launch / run+fetch / free / total of a call whose create_job filled phases 0-2
 void record_call_timing(double t0, double t1, double t2, double t3) {
     g_timing[3] = t2 - t1;
@@ -852,6 +932,7 @@ int bnpp_ctx_create(int device, bnpp_ctx **out) {
 int bnpp_ctx_destroy(bnpp_ctx *ctx) {
     if (!ctx) return BNPP_OK;
     (void)hipSetDevice(ctx->c.device);
+    evict_cached_job(ctx);
     if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
     if (ctx->c.lane_stream) (void)hipStreamDestroy(ctx->c.lane_stream);
     ctx->srcs.clear();
@@ -867,6 +948,7 @@ int bnpp_ctx_trim(bnpp_ctx *ctx) {
     if (!lk.owns_lock()) return set_err(BNPP_ERR_INVALID, "a call on this context is running");
     (void)hipSetDevice(ctx->c.device);
     (void)hipDeviceSynchronize();
+    evict_cached_job(ctx);
     {
         std::lock_guard<std::mutex> g(ctx->src_mu);
         ctx->srcs.clear();
@@ -1271,18 +1353,23 @@ int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
                    double *uptime_ms) {
     BNPP_GUARD_BEGIN
     double t0 = now_ms();
-    std::unique_ptr<bnpp_job> job;
-    std::unique_lock<std::mutex> lk;
-    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
-    int rc = create_job(ctx, m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype, job, 0, 1,
-                        lk.owns_lock());
+    if (!ctx || !m) return set_err(BNPP_ERR_INVALID, "null context or model");
+    bnpp_job *job = nullptr;
+    std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
+    const bool cache_ok = lk.owns_lock();
+    const uint64_t key = cache_ok ? call_key(m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype,
+                                             0, 1, memory_budget(ctx, true)) : 0;
+    int rc = oneshot_job(ctx, cache_ok, key, [&](std::unique_ptr<bnpp_job> &j) {
+        return create_job(ctx, m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype, j, 0, 1,
+                          cache_ok);
+    }, job);
     const double t1 = now_ms();
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     const double t2 = now_ms();
     double lz = 0, zz = 0;
-    if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, &lz, &zz);
+    if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, &lz, &zz);
     const double t3 = now_ms();
-    if (job) destroy_job(job.release());
+    oneshot_done(ctx, cache_ok, key, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (rc) return rc;
     if (log10_z) *log10_z = lz;
@@ -1297,17 +1384,22 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     BNPP_GUARD_BEGIN
     if (!out) return set_err(BNPP_ERR_INVALID, "null output");
     double t0 = now_ms();
-    std::unique_ptr<bnpp_job> job;
-    std::unique_lock<std::mutex> lk;
-    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
-    int rc = create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, job, 0, 1,
-                        lk.owns_lock());
+    if (!ctx || !m) return set_err(BNPP_ERR_INVALID, "null context or model");
+    bnpp_job *job = nullptr;
+    std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
+    const bool cache_ok = lk.owns_lock();
+    const uint64_t key = cache_ok ? call_key(m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets,
+                                             dtype, 0, 1, memory_budget(ctx, true)) : 0;
+    int rc = oneshot_job(ctx, cache_ok, key, [&](std::unique_ptr<bnpp_job> &j) {
+        return create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, j, 0, 1,
+                          cache_ok);
+    }, job);
     const double t1 = now_ms();
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     const double t2 = now_ms();
-    if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr);
+    if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, out, nullptr);
     const double t3 = now_ms();
-    if (job) destroy_job(job.release());
+    oneshot_done(ctx, cache_ok, key, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (std::getenv("BNPP_TIMING"))
         std::fprintf(stderr, "[bnpp] marginals: create %.1f ms, launch %.1f ms, run+fetch %.1f ms, free %.1f ms\n",
@@ -1331,18 +1423,23 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
     BNPP_GUARD_BEGIN
     if (!out) return set_err(BNPP_ERR_INVALID, "null output");
     double t0 = now_ms();
+    if (!ctx || !m) return set_err(BNPP_ERR_INVALID, "null context or model");
     const bool timing = std::getenv("BNPP_TIMING") != nullptr;
-    std::unique_ptr<bnpp_job> job;
-    std::unique_lock<std::mutex> lk;
-    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
-    int rc = create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job,
-                        part, n_parts, lk.owns_lock());
+    bnpp_job *job = nullptr;
+    std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
+    const bool cache_ok = lk.owns_lock();
+    const uint64_t key = cache_ok ? call_key(m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets,
+                                             targets, dtype, part, n_parts, memory_budget(ctx, true)) : 0;
+    int rc = oneshot_job(ctx, cache_ok, key, [&](std::unique_ptr<bnpp_job> &j) {
+        return create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, j,
+                          part, n_parts, cache_ok);
+    }, job);
     const double t1 = now_ms();
     if (rc == BNPP_OK) rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     const double t2 = now_ms();
-    if (rc == BNPP_OK) rc = job_results(job.get(), ctx->c.stream, out, nullptr, owned);
+    if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, out, nullptr, owned);
     const double t3 = now_ms();
-    if (job) destroy_job(job.release());
+    oneshot_done(ctx, cache_ok, key, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (timing)
         std::fprintf(stderr, "[bnpp] tree marginals: create %.1f ms, launch %.1f ms, run+fetch %.1f ms, free %.1f ms\n",

@@ -45,6 +45,7 @@ for name, res, args in [
     ("rc_micro_bucket", C.c_double, [_I, _I, _I, _DP]),
     ("rc_sum_product", _I, [_P, _I, C.c_double, _DP, _IP, _DP]),
     ("rc_ordering", _I, [_P, _I, C.POINTER(_P), _I, _IP, _I, _IP]),
+    ("rc_variable_elimination", _P, [_P, _I, _IP, _I, C.POINTER(_P), _I]),
 ]:
     f = getattr(_lib, name)
     f.restype = res
@@ -183,6 +184,15 @@ class Model:
         out = (C.c_int * max(len(variables), 1))()
         w = _lib.rc_ordering(self.h, nf, fs, len(variables), _ints(variables), HEURISTICS[heuristic], out)
         return list(out[:len(variables)]), w
+
+    def variable_elimination(self, variables: Sequence[int], heuristic: str = "given") -> "Factor":
+        """BN::variable_elimination (model.cpp:348-446) over the model's own
+        factors, eliminating `variables` (in this order with "given")."""
+        nf = _lib_model_nf(self.h)
+        fs = C.cast(C.c_void_p(_model_factors(self.h)), C.POINTER(_P))
+        variables = list(variables)
+        return Factor(_lib.rc_variable_elimination(self.h, len(variables), _ints(variables), nf, fs,
+                                                   HEURISTICS[heuristic]))
 
     def marginal(self, target: int, evidence=None, heuristic: str = "mf"):
         n, v, x = self._ev(evidence)

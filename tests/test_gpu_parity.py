@@ -561,3 +561,52 @@ def test_source_cache_never_serves_another_model(ctx):
         outs.append(z1)
         del m
     assert outs[0] == outs[2] and outs[0] != outs[1]
+
+
+def test_variable_elimination_large_result_vs_oracle(ctx):
+    """BN::variable_elimination leaving 22 of a 6x7 grid's variables: a
+    4-Mi-entry result table, copied out of the arena by several workgroups
+    (launch.hip copy_tables_kernel); scope in the reference's order and
+    values (scaled by 2^exp2, exact) equal to the oracle's."""
+    from bnpp import synth
+    d = synth.ising_grid(6, 7, seed=21)
+    m = bnpp.Model.from_dict(d)
+    elim = list(range(0, 42, 2))[:20]
+    scope, vals, e2 = bnpp.variable_elimination(ctx, m, elim, "given", bnpp.F64, cap_values=1 << 23)
+    ref = refcpu.Model.from_dict(d).variable_elimination(elim, "given")
+    assert scope == ref.scope
+    rv = ref.values
+    assert len(vals) == len(rv) == 1 << 22
+    assert all(math.ldexp(a, e2) == b for a, b in zip(vals, rv))
+
+
+def test_job_cache_reuses_only_identical_calls(ctx):
+    """The context keeps the last one-shot job (capi.cpp oneshot_job): an
+    identical call relaunches it (no planning: plan_ms 0), any difference --
+    evidence, dtype, order, a BNPP_* knob -- plans afresh; results always
+    equal the oracle's."""
+    from bnpp import synth
+    import os
+    d = synth.ising_grid(6, 6, seed=4)
+    m = bnpp.Model.from_dict(d)
+    rm = refcpu.Model.from_dict(d)
+    z0 = bnpp.partition(ctx, m, {}, "mf", bnpp.F64)[1]
+    z1 = bnpp.partition(ctx, m, {}, "mf", bnpp.F64)[1]
+    assert bnpp.last_timing()["plan_ms"] == 0.0
+    assert z0 == z1 == rm.partition({}, "mf")[0]
+    ze = bnpp.partition(ctx, m, {3: 1}, "mf", bnpp.F64)[1]
+    assert bnpp.last_timing()["plan_ms"] > 0.0
+    assert ze == rm.partition({3: 1}, "mf")[0]
+    os.environ["BNPP_NO_CHAIN"] = "1"
+    try:
+        zk = bnpp.partition(ctx, m, {3: 1}, "mf", bnpp.F64)[1]
+        assert bnpp.last_timing()["plan_ms"] > 0.0
+    finally:
+        del os.environ["BNPP_NO_CHAIN"]
+    assert zk == ze
+    mg = bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64)[0]
+    mg2 = bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64)[0]
+    assert bnpp.last_timing()["plan_ms"] == 0.0 and mg == mg2
+    want, _ = rm.marginals({}, "mf")
+    for t in range(m.n_vars):
+        assert all(abs(a - b) <= 1e-12 for a, b in zip(mg[t], want[t]))
