@@ -202,8 +202,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     constexpr int ROWB = N * 4 + 16;                       // image row stride (bytes)
     constexpr int HB = 8 - F;                              // phase 2: bits of h (n-digits 0-3 local)
     constexpr int SB = F - 4;                              // phase 2: bits of the slot combo (slots 4..F-1)
-    constexpr int RPW = kSplitRows / W;                    // backward: input rows loaded per wave
-    constexpr int CPR = N / 4;                             // backward: 16-B chunks per row
+    constexpr int CPR = N / 4;                             // 16-B chunks per row
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
     T *xch = reinterpret_cast<T *>(dyn + kRedBytes);
@@ -212,6 +211,13 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // digit of slot p (4 <= p < F) in phase 1: bit (F-1-p) of w
     auto wdig = [&](int p) { return (w >> (F - 1 - p)) & 1; };
+    // the tile's 64 rows are 16 * N contiguous bytes; row traffic (backward
+    // loads, forward stores) goes in 4 instructions per lane, instruction `it`
+    // of the whole workgroup covering W contiguous KiB: 16-B chunk
+    // it * 64 W + 64 w + lane (row 16 it + w at F = 8), not 4 consecutive rows
+    // per wave (forward 6.06 -> 5.97 ms, backward 5.81 -> 5.69-5.73 ms in
+    // tools/bwdprobe.hip, profiles/r04_bwdprobe.jsonl)
+    auto chunk = [&](int it) { return it * 64 * W + 64 * w + lane; };
 
     int cur = -1;
     int64_t cur_begin = 0, cur_end = 0;
@@ -320,8 +326,8 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             const T *big = c.big + tin;
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
-                const int q = it * 64 + lane;
-                const int rw = w * RPW + q / CPR, ch = q % CPR;
+                const int q = chunk(it);
+                const int rw = q / CPR, ch = q % CPR;
                 const vec_t<T, 4> v = vload<4, kNtLoad, true>(big + (int64_t)rw * N + 4 * ch);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) rg[4 * it + k] = v[k];
@@ -340,13 +346,13 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 rg[e] = gload(reinterpret_cast<const T *>(reinterpret_cast<const char *>(sp) + lob));
             }
         } else {
-            // 64 input rows of N contiguous values (slot 0 fastest): wave w loads
-            // its RPW rows with 16-B loads (4 per lane)
+            // 64 input rows of N contiguous values (slot 0 fastest), 16-B loads
+            // (4 per lane)
             const T *big = c.big;
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
-                const int q = it * 64 + lane;
-                const int rw = w * RPW + q / CPR, ch = q % CPR;
+                const int q = chunk(it);
+                const int rw = q / CPR, ch = q % CPR;
                 const int64_t ro = __shfl(in_off, rw, 64);  // row rw's input offset (held by lane rw)
                 const vec_t<T, 4> v = vload<4, kNtLoad, true>(big + ro + 4 * ch);
 #pragma unroll
@@ -379,8 +385,8 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             // rows through the image, then this lane's 16 entries (slots 4.. = w)
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
-                const int q = it * 64 + lane;
-                const int rw = w * RPW + q / CPR, ch = q % CPR;
+                const int q = chunk(it);
+                const int rw = q / CPR, ch = q % CPR;
                 *reinterpret_cast<vec_t<T, 4> *>(img + rw * ROWB + 16 * ch) =
                     vec_t<T, 4>{t[4 * it], t[4 * it + 1], t[4 * it + 2], t[4 * it + 3]};
             }
@@ -443,13 +449,13 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                     vec_t<T, 4>{t[4 * c4], t[4 * c4 + 1], t[4 * c4 + 2], t[4 * c4 + 3]};
             lds_barrier();
             // the 64 rows are one contiguous block of 64 * N entries (planner-checked):
-            // wave w stores its 4 KiB share, 1 KiB per instruction
+            // 1 KiB per wave-instruction (chunk())
             T *out = c.out + (DENSE ? tout : __shfl(out_off, 0, 64));
             // (tiles are whole: the planner requires rest dim 0 to be a multiple of 64)
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
-                const int q = w * 256 + it * 64 + lane;    // 16-B chunk within the block
-                const int rw = q / (N / 4), ch = q % (N / 4);
+                const int q = chunk(it);                   // 16-B chunk within the block
+                const int rw = q / CPR, ch = q % CPR;
                 const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4> *>(img + rw * ROWB + 16 * ch);
                 vstore<4, kNtStore, true>(out + 4 * (int64_t)q, v);
             }
