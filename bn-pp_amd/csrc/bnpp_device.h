@@ -20,7 +20,8 @@
 namespace bnpp {
 
 constexpr int kMaxIn = 8;          // inputs per fused launch; longer chains are split
-constexpr int kMaxDescIn = 9;      // descriptor slots: a fused run of 8 buckets has 8 G tables + the message
+constexpr int kMaxDescIn = 10;     // descriptor slots: a fused run of 8 buckets has 8 G tables + the message
+                                   // (+ the forward message of a fused belief, kChainBel)
 constexpr int kSplitRowsHost = 64; // rest entries per workgroup of the split chain forms (chainsplit.cuh)
 // split forms: each G_j staged in LDS packed, 8 entries [q][n][x] per base
 // offset (one 32-B pair of 16-B reads per bucket); LDS per workgroup: the
@@ -52,6 +53,10 @@ enum BucketFlags : int32_t {
     kChainLo32 = 8,    // chain form: the streamed side (forward input / backward output)
                        // is linear in the thread index, so one wave's accesses are a
                        // uniform base + a 32-bit lane offset (saddr addressing)
+    kChainBel = 32,    // dense backward split run that also forms a delivery's belief:
+                       // aux_out[r] = sum over the run's slot combination s (ascending)
+                       // of lam[r + s S] * out[r + s S] (lam: in_table[n_in], laid out
+                       // as the run's output), unscaled (exp2 = exp2(lam) + exp2(out))
 };
 
 // Each thread evaluates a V1 x V2 register tile of the output: V1 entries of
@@ -81,6 +86,8 @@ struct BucketDesc {
     // 32 B: each lane then stores 16 B and a wave's store is one contiguous
     // 1-KiB run instead of 16-B pieces at a 32-B stride)
     int32_t lanes;
+    // kChainBel: the belief table the run also writes
+    int32_t aux_out;
 };
 
 // arguments of one level launch (a group of buckets of one kernel variant)

@@ -473,10 +473,12 @@ void arena_profile(const Schedule &s, int eb, const char *path) {
         double moved = 0;
         for (int k = g.begin; k < g.end; ++k) {
             const BucketDesc &d = s.descs[k];
-            int tabs[kMaxDescIn + 1];
+            int tabs[kMaxDescIn + 2];
             int nt = 0;
-            for (int i = 0; i < d.n_in && i < kMaxDescIn; ++i) tabs[nt++] = d.in_table[i];
+            const int n_read = d.n_in + ((d.flags & kChainBel) ? 1 : 0);
+            for (int i = 0; i < n_read && i < kMaxDescIn; ++i) tabs[nt++] = d.in_table[i];
             tabs[nt++] = d.out_table;
+            if (d.flags & kChainBel) tabs[nt++] = d.aux_out;
             for (int i = 0; i < nt; ++i) {
                 const int t = tabs[i];
                 if (t < 0) continue;

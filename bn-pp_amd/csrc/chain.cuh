@@ -149,11 +149,12 @@ __device__ __forceinline__ int chain_stage(const BucketDesc &d, TableMeta *meta,
     __syncthreads();
 #pragma unroll
     for (int i = 1; i < kMaxDescIn; ++i) {
-        if (i >= d.n_in) break;
-        const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
-        const int off = d.in_lds_off[i], span = d.in_span[i];
-        const T sc = ldexp_t(T(1), s[i]);
-        for (int e = threadIdx.x; e < span; e += kBlock) small[off + e] = gload(src + e) * sc;
+        if (i < d.n_in) {                                  // uniform (a guard, not a break: the loop unrolls)
+            const T *src = static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i];
+            const int off = d.in_lds_off[i], span = d.in_span[i];
+            const T sc = ldexp_t(T(1), s[i]);
+            for (int e = threadIdx.x; e < span; e += kBlock) small[off + e] = gload(src + e) * sc;
+        }
     }
     __syncthreads();
     return left;

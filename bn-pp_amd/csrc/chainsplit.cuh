@@ -126,6 +126,9 @@ struct SplitState {
     int d_shift;
     int64_t d_in1, d_out1, d_slab;
     int32_t d_g1[F];
+    // kChainBel (dense backward runs): the forward message and the belief table
+    const float *lam;
+    float *bel;
 };
 
 template <int F, int DEP, bool DENSE, int FORM>
@@ -178,6 +181,14 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
     c.big = static_cast<const float *>(meta[d.in_table[0]].ptr);
     c.out = static_cast<float *>(meta[d.out_table].ptr);
     c.left = 0;
+    c.lam = nullptr;
+    c.bel = nullptr;
+    if constexpr (DENSE && FORM == kChainBwd) {
+        if (d.flags & kChainBel) {
+            c.lam = static_cast<const float *>(meta[d.in_table[d.n_in]].ptr) + d.in_base[d.n_in];
+            c.bel = static_cast<float *>(meta[d.aux_out].ptr);
+        }
+    }
 }
 
 // workgroup barrier for the LDS exchange only: waits for this wave's LDS
@@ -223,6 +234,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     int64_t cur_begin = 0, cur_end = 0;
     SplitState<F, DEP> c;
     T lmax = T(0);
+    T bmax = T(0);                                         // kChainBel: the belief's running max (wave 0)
 
     // bucket of virtual block vb: state, published exponent, G tables in LDS
     auto setup = [&](int64_t vb) {
@@ -236,7 +248,12 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         c.left = chain_fold<T>(d, meta, fs);
         // exp2 of the output: the inputs' exp2 and max exponents, plus the
         // share of the rescale not folded (chain_fold)
-        if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = chain_exp2<T>(d, meta) + c.left;
+        if (vb == cur_begin && threadIdx.x == 0) {
+            const int64_t e_out = chain_exp2<T>(d, meta) + c.left;
+            meta[d.out_table].exp2 = e_out;
+            // the belief is stored unscaled: true value = stored * 2^(exp2(lam) + exp2(out))
+            if (c.bel) meta[d.aux_out].exp2 = meta[d.in_table[d.n_in]].exp2 + e_out;
+        }
         lds_barrier();                                     // the previous bucket's tables are no longer read
         // G_j packed: entry (o, q, n, x) at 8 o + 4 q + 2 n + x holds G_j[o + q
         // gsq + n gsn + x gsj] * 2^fs (gmask is all ones: G_j is input j + 1)
@@ -374,13 +391,53 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             if (m > T(0) && __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mine) atomicMax(mb, mine);
         }
         lmax = T(0);
+        if constexpr (FORM == kChainBwd && DENSE) {
+            if (c.bel && w == 0 && (c.flags & kTrackMax)) {     // only wave 0 forms beliefs
+                const T bm = wave_max(bmax);
+                using U = typename FBits<T>::U;
+                U *mb = reinterpret_cast<U *>(&meta[descs[cur].aux_out].maxbits);
+                if (lane == 0 && bm > T(0)) atomicMax(mb, FBits<T>::bits(bm));
+            }
+        }
+        bmax = T(0);
     };
 
     // one tile: the 16 values per lane in t, this lane's rest entry decoded
     // Barriers per tile: forward  [phase 1, xch write] B [xch read, phase 2, image write] B [image read];
     // backward [image write] B [image read, phase 1, xch write] B [xch read, phase 2].  A wave past one
     // of them knows every wave has finished the previous tile's reads of the region it writes next.
+    // slab of entry e (backward dense runs): the wave's digits (wsl) | e's (sl)
+    auto slab_w = [&]() {
+        int wsl = 0;
+#pragma unroll
+        for (int p = 0; p < 4 - HB; ++p) wsl |= (((w << HB) >> (3 - p)) & 1) << p;
+        return wsl;
+    };
+    auto slab_e = [&](int e) {
+        int sl = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) sl |= ((e >> (3 - b)) & 1) << (4 - HB + b);
+        return sl;
+    };
+    // kChainBel: the forward message at this lane's 16 output positions of the
+    // tile whose rest offset is `to` (the same scattered addresses as the
+    // stores), loaded at the start of the tile so they arrive behind its
+    // exchange.  They are most of a fused run's extra time (10.9 ms per run
+    // against 6.9 ms with the loads removed and 6.3 ms unfused); loading them
+    // a tile ahead was slower still (8.3 ms average over all backward runs
+    // against 7.9 ms, 128 VGPRs) -- profiles/r04_belief_fusion_ab.txt
+    float lv[16];
+    auto load_lam = [&](int64_t to) {
+        if constexpr (FORM == kChainBwd && DENSE) {
+            const float *lb = c.lam + to + (int64_t)slab_w() * c.d_slab + lane;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) lv[e] = gload(lb + (int64_t)slab_e(e) * c.d_slab);
+        }
+    };
     auto run_tile = [&](float (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
+        if constexpr (FORM == kChainBwd && DENSE) {
+            if (c.bel) load_lam(tout);
+        }
         if constexpr (FORM == kChainBwd) {
             // rows through the image, then this lane's 16 entries (slots 4.. = w)
 #pragma unroll
@@ -464,16 +521,34 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             if constexpr (DENSE) {
                 // output slab of n-digits (slot p at S << p): e's local bits are
                 // slots 4-HB .. F-1 (MSB first), the wave's digits the others
-                int wsl = 0;
-#pragma unroll
-                for (int p = 0; p < 4 - HB; ++p) wsl |= (((w << HB) >> (3 - p)) & 1) << p;
+                const int wsl = slab_w();
                 T *wb = c.out + tout + (int64_t)wsl * c.d_slab + lane;
 #pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    int sl = 0;
+                for (int e = 0; e < 16; ++e) store_n<T, 1, kNtStore, true>(wb + (int64_t)slab_e(e) * c.d_slab, &t[e]);
+                if (c.bel) {
+                    // belief of rest entry r = lane: lam * pi per slab s into row r
+                    // of the image (free: every wave read its rows before the
+                    // exchange barrier), then one wave adds each row's 2^F
+                    // products in slab order -- the unfused bucket's order
+                    // (p = lam * pi; acc = 0; acc += p for s = 0, 1, ...)
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) sl |= ((e >> (3 - b)) & 1) << (4 - HB + b);
-                    store_n<T, 1, kNtStore, true>(wb + (int64_t)sl * c.d_slab, &t[e]);
+                    for (int e = 0; e < 16; ++e)
+                        *reinterpret_cast<T *>(img + lane * ROWB + 4 * (wsl | slab_e(e))) = lv[e] * t[e];
+                    lds_barrier();
+                    if (w == 0) {
+                        T acc = T(0);
+#pragma unroll 4
+                        for (int c4 = 0; c4 < N / 4; ++c4) {
+                            const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4> *>(img + lane * ROWB + 16 * c4);
+                            acc = acc + v[0];
+                            acc = acc + v[1];
+                            acc = acc + v[2];
+                            acc = acc + v[3];
+                        }
+                        store_n<T, 1, kNtStore, true>(c.bel + tout + lane, &acc);
+                        bmax = fmaxf(bmax, acc);
+                    }
+                    lds_barrier();                         // the image is the next tile's again
                 }
             } else {
                 const int64_t w0 = readfirstlane64(out_off);

@@ -230,7 +230,8 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     int ni = 1;
     for (int j = 0; j < F; ++j)
         if ((b.chain_gmask >> j) & 1) gidx[j] = ni++;
-    if (ni != (int)b.in.size() || ni > kMaxDescIn) return fail("chain: G tables do not match the mask");
+    const int nb = b.bel_table >= 0 ? 1 : 0;          // the belief's forward message follows the G tables
+    if (ni + nb != (int)b.in.size() || ni + nb > kMaxDescIn) return fail("chain: G tables do not match the mask");
     if (ni > kMaxIn && !split_ok) return fail("chain: more than 8 inputs need the split form");
     auto stride_of = [](const View &v, int var) -> int64_t {
         for (size_t i = 0; i < v.vars.size(); ++i)
@@ -398,6 +399,16 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         V = chain_fwd_v(N, eb);
     }
     if (!chain_supported(eb, chain_key(form, K, F, dep))) return fail("chain: shape not instantiated");
+    if (nb) {
+        // the belief (kChainBel): the dense backward form, the output's rest one
+        // dense block below the slot stride S (belief entry r = output rest
+        // offset), the forward message laid out exactly as the output
+        if (form != kChainBwdSD) return fail("chain: a fused belief needs the dense backward form");
+        const View &lam = b.in[ni];
+        bool same = lam.vars.size() == b.out_vars.size() && rest == os[0];
+        for (size_t i = 0; same && i < b.out_vars.size(); ++i) same = stride_of(lam, b.out_vars[i]) == ostr[i];
+        if (!same) return fail("chain: the belief's forward message is not laid out as the run's output");
+    }
     if (std::getenv("BNPP_DEBUG_CHAIN"))
         std::fprintf(stderr, "[chain] run form %d K=%d F=%d dep %d V=%d rest %lld\n", form, K, F, dep, V, (long long)rest);
     d = BucketDesc{};
@@ -409,7 +420,8 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
     d.n_dims = (int)md.size();
     d.k = K;
     d.out_table = b.out_table;
-    d.flags = kScale | kTrackMax;
+    d.flags = kScale | kTrackMax | (nb ? kChainBel : 0);
+    d.aux_out = nb ? b.bel_table : 0;
     d.big = -1;
     d.chain = F | (b.chain_gmask << 8) | (form << 16) | (dep << 20);
     {
@@ -439,6 +451,10 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
             d.in_lds_off[i] = lo;
             lo += chain_split_form(form) ? (int32_t)(sp * kSplitPack) : (int32_t)((sp + 3) & ~3);
         }
+    }
+    if (nb) {
+        d.in_table[ni] = b.in[ni].table;
+        d.in_base[ni] = b.in[ni].base;
     }
     d.small_elems = lo;
     if ((int64_t)lo * eb > (chain_split_form(form) ? split_g_budget_bytes(F) : kStreamLdsBudget))
@@ -1015,6 +1031,45 @@ struct PlanBuilder {
         p.width = std::max(p.width, (int)b.out_vars.size());
         p.buckets.push_back(b);
         return b.out_table;
+    }
+    // A delivery's belief folded into the backward run that just made its
+    // message pi (kChainBel, chainsplit.cuh): the run also reads lam (laid out
+    // as pi) and writes bel[r] = sum over its slot combinations s, ascending,
+    // of lam[r + s S] * pi[r + s S] -- the separate belief pass re-read all of
+    // pi (17 GB per delivery on the 32x32 sweep) and lam.  slow: the summed
+    // (slowest) variables, which must be the run's slots.  Returns the belief
+    // table, or -1 (the caller then emits the belief bucket).
+    int attach_belief(const View &pi, const View &lam, const std::vector<int> &slow) {
+        const char *off = std::getenv("BNPP_NO_BEL_FUSE");
+        if (p.buckets.empty() || (off && *off == '1')) return -1;
+        BucketSpec &b = p.buckets.back();
+        const int F = (int)b.chain_n.size();
+        if (b.chain_x.empty() || b.bel_table >= 0 || b.out_table != pi.table || pi.base != 0 || lam.base != 0 ||
+            (int)slow.size() != F || (int)pi.vars.size() <= F || lam.vars != pi.vars || lam.strides != pi.strides ||
+            lam.table < p.n_src || level[lam.table] >= b.level)
+            return -1;
+        for (int i = 0; i < F; ++i)
+            if (!contains(slow, pi.vars[i]) || !contains(b.chain_n, pi.vars[i])) return -1;
+        const std::vector<int> kv(pi.vars.begin() + F, pi.vars.end());
+        if (canon(kv) != kv) return -1;
+        {
+            BucketSpec t = b;                           // the run's descriptor with the belief attached
+            t.in.push_back(lam);
+            t.bel_table = pi.table;
+            BucketDesc d;
+            std::vector<int64_t> pool;
+            std::string why;
+            if (!build_desc(t, cards, chain_eb == 8 ? 2 : 4, d, pool, &why)) {
+                if (std::getenv("BNPP_DEBUG_CHAIN")) std::fprintf(stderr, "[chain] belief not fused: %s\n", why.c_str());
+                return -1;
+            }
+        }
+        b.in.push_back(lam);
+        b.bel_table = new_msg(kv);
+        level[b.bel_table] = b.level;
+        p.entries += (double)table_size(pi.vars, cards);
+        p.elems_moved += (double)table_size(lam.vars, cards) + (double)p.msgs[b.bel_table - p.n_src].size;
+        return b.bel_table;
     }
     // first bucket (by elimination rank >= from) whose variable is in `vars`
     int first_bucket(const std::vector<int> &vars, int from) const {
@@ -1655,9 +1710,13 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 mark(mit->second);
                 int tb = -1;                                   // one pass: sum the slow vars
                 if (slow_j.size() >= 2) {
-                    std::vector<View> mg = bel;
-                    int vv = B.merge_group(mg, slow_j);
-                    if (vv >= 0) tb = B.emit(mg, vv, false);
+                    // folded into the backward run that made pi_j, when it can be
+                    if (sbits == 0 && bel.size() == 2) tb = B.attach_belief(bel[1], bel[0], slow_j);
+                    if (tb < 0) {
+                        std::vector<View> mg = bel;
+                        int vv = B.merge_group(mg, slow_j);
+                        if (vv >= 0) tb = B.emit(mg, vv, false);
+                    }
                 } else {
                     tb = B.emit(bel, slow_j.empty() ? -1 : slow_j[0], false);
                 }
@@ -1874,6 +1933,7 @@ int64_t plan_peak_bytes(const VEPlan &p, int elem_bytes) {
     std::vector<int> born(nt, 0), last(nt, -1);
     for (const BucketSpec &b : p.buckets) {
         born[b.out_table] = b.level;
+        if (b.bel_table >= 0) born[b.bel_table] = b.level;
         for (const View &v : b.in) last[v.table] = std::max(last[v.table], b.level);
     }
     if (p.result_table >= 0) last[p.result_table] = p.n_levels + 1;
@@ -1973,6 +2033,7 @@ int64_t plan_arena_bytes(const VEPlan &p, int elem_bytes) {
     std::vector<int> born(nt, 0), last(nt, -1);
     for (const BucketSpec &b : p.buckets) {
         born[b.out_table] = b.level;
+        if (b.bel_table >= 0) born[b.bel_table] = b.level;
         for (const View &v : b.in) last[v.table] = std::max(last[v.table], b.level);
     }
     std::vector<char> keep(nt, 0);
@@ -2078,6 +2139,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                     }
                 }
                 th[b.out_table - p.n_src] = {h1, h2};
+                if (b.bel_table >= 0) th[b.bel_table - p.n_src] = {h1 ^ 0x5bd1e9955bd1e995ull, h2 + 0x27d4eb2f165667c5ull};
             }
             for (size_t i = 0; i < p.msgs.size(); ++i) {
                 const int g = msg_base[pi] + (int)i;
@@ -2152,6 +2214,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         for (const BucketSpec &b : plans[pi]->buckets) {
             if (!kept(pi, b)) continue;
             born[remap(pi, b.out_table)] = b.level;
+            if (b.bel_table >= 0) born[remap(pi, b.bel_table)] = b.level;
             for (const View &v : b.in) {
                 int *lt = &last[remap(pi, v.table)];
                 int cur = __atomic_load_n(lt, __ATOMIC_RELAXED);
@@ -2171,6 +2234,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         for (const BucketSpec &b : plans[pi]->buckets) {
             if (!kept(pi, b)) continue;
             lane_of[remap(pi, b.out_table)] = b.lane;
+            if (b.bel_table >= 0) lane_of[remap(pi, b.bel_table)] = b.lane;
             n_lanes = std::max(n_lanes, b.lane + 1);
         }
     if (n_lanes > 1)
@@ -2309,6 +2373,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                    plans[it.plan]->msgs[b.out_table - s.n_src].size <= simple_max;
         for (View &v : b.in) v.table = remap(it.plan, v.table);
         b.out_table = remap(it.plan, b.out_table);
+        if (b.bel_table >= 0) b.bel_table = remap(it.plan, b.bel_table);
         if (b.xchg) {                        // an exchange step: the executor's, no kernel descriptor
             it.d = BucketDesc{};
             it.d.n_in = (int)b.in.size();
@@ -2384,6 +2449,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 }
                 std::fprintf(stderr, " slots:");
                 for (int q = 0; q < F; ++q) std::fprintf(stderr, " %lld/%lld", (long long)pl[2 * q], (long long)pl[2 * q + 1]);
+                if (d.flags & kChainBel) std::fprintf(stderr, " belief: %d x %d -> %d", d.in_table[d.n_in], d.out_table, d.aux_out);
                 std::fprintf(stderr, "\n");
             } else if (dump && g.variant >= kXchgKeyBase) {
                 std::fprintf(stderr, "L%d xchg kind=%d mode=%d blocks=%d tables:%d->%d entries=%lld\n", g.level,

@@ -69,6 +69,10 @@ struct BucketSpec {
     // in[1..] are the G tables of the buckets whose bit is set in chain_gmask
     std::vector<int> chain_x, chain_n;
     int chain_gmask = 0;
+    // a dense backward split run may also form a delivery's belief (kChainBel):
+    // its table here, the forward message it multiplies by the last entry of
+    // `in` (after the G tables)
+    int bel_table = -1;
     bool divide = false;            // Factor::divide: in[0] / in[1] (generic kernel, no sum)
     // build_schedule: a small bucket of a level with several kernel variants
     // runs in the level's one generic 1x1 launch (launch count, not bandwidth,

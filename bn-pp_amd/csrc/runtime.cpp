@@ -185,7 +185,8 @@ int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Execut
             const Schedule::Group &g = sc.groups[gi];
             for (int k = g.begin; k < g.end; ++k) {
                 const BucketDesc &d = sc.descs[k];
-                for (int i = 0; i < d.n_in && i < kMaxDescIn; ++i) {
+                const int n_read = d.n_in + ((d.flags & kChainBel) ? 1 : 0);   // + a fused belief's forward message
+                for (int i = 0; i < n_read && i < kMaxDescIn; ++i) {
                     const int t = d.in_table[i], pg = t >= 0 ? prod[t] : -1;
                     if (pg < 0 || sc.groups[pg].lane == g.lane) continue;
                     if (ex.g_record[pg] < 0) ex.g_record[pg] = n_ev++;
@@ -193,7 +194,10 @@ int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Execut
                     if (std::find(w.begin(), w.end(), ex.g_record[pg]) == w.end()) w.push_back(ex.g_record[pg]);
                 }
             }
-            for (int k = g.begin; k < g.end; ++k) prod[sc.descs[k].out_table] = gi;
+            for (int k = g.begin; k < g.end; ++k) {
+                prod[sc.descs[k].out_table] = gi;
+                if (sc.descs[k].flags & kChainBel) prod[sc.descs[k].aux_out] = gi;
+            }
         }
         ex.events.assign(n_ev, nullptr);
         for (hipEvent_t &e : ex.events)

@@ -421,6 +421,54 @@ def test_split_runs_peaked_potentials(ctx, capfd, rows, cols, log2_eps):
         assert _close(res[0][1][t], want[t], 1e-5), (t, res[0][1][t], want[t])
 
 
+def _two_grids(a, b):
+    n = len(a["cards"])
+    return {"type": "MARKOV", "cards": a["cards"] + b["cards"],
+            "scopes": a["scopes"] + [[v + n for v in s] for s in b["scopes"]], "values": a["values"] + b["values"]}
+
+
+@pytest.mark.parametrize("model", ["ising", "peaked", "two"])
+def test_fused_beliefs_identical_to_belief_passes(ctx, capfd, model):
+    """Deliveries whose belief sums the slots of the backward run that made
+    its message (kChainBel: 16x6 column sweeps with 2^8-entry kept sets, so a
+    belief sums 8 binary variables) are formed inside that run -- it also
+    reads the forward message and adds lam * pi over its 256 slot
+    combinations in slab order -- instead of a separate pass over lam and pi.
+    The belief is stored unscaled (its exp2 carries the inputs'), so the tree
+    marginals are bit-identical to the separate belief passes
+    (BNPP_NO_BEL_FUSE), to one-thread runs and to one bucket per launch, and
+    within fp32 rounding of the fp64 per-target engine; peaked potentials
+    (every bucket product <= 2^-10) and two disconnected grids included."""
+    if model == "ising":
+        d = synth.ising_grid(16, 6, seed=31)
+    elif model == "peaked":
+        d = synth.peaked_grid(16, 6, log2_eps=10, seed=32)
+    else:
+        d = _two_grids(synth.ising_grid(16, 6, seed=33), synth.ising_grid(16, 6, seed=34))
+    m = bnpp.Model.from_dict(d)
+    col = [i * 6 + j for j in range(6) for i in range(16)]
+    order = col if model != "two" else col + [v + 96 for v in col]
+    knobs = [{"BNPP_DUMP_PLAN": "1"}, {"BNPP_NO_BEL_FUSE": "1"}, {"BNPP_NO_SPLIT": "1"}, {"BNPP_NO_CHAIN": "1"}]
+    res = []
+    for kn in knobs:
+        os.environ.update(kn)
+        os.environ.update({"BNPP_KEEP_LOG2": "8", "BNPP_TREE_SLOTS": "3"})
+        capfd.readouterr()
+        try:
+            res.append(bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F32, order=order)[0])
+        finally:
+            for key in list(kn) + ["BNPP_KEEP_LOG2", "BNPP_TREE_SLOTS"]:
+                del os.environ[key]
+        if "BNPP_DUMP_PLAN" in kn:
+            fused = [ln for ln in capfd.readouterr().err.splitlines() if " belief: " in ln]
+            assert len(fused) >= (8 if model != "two" else 16), len(fused)
+    for out in res[1:]:
+        assert out == res[0]
+    want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    for t in range(m.n_vars):
+        assert _close(res[0][t], want[t], 1e-5), (t, res[0][t], want[t])
+
+
 @pytest.mark.parametrize("keep,slow,rows", [(3, 13, 12), (5, 13, 12), (7, 2, 12), (9, 4, 12), (13, 13, 14)])
 def test_tree_chain_kept_sets_match(ctx, keep, slow, rows):
     """Deliveries from kept sets smaller than the separators (the 32x32 path:
