@@ -469,6 +469,40 @@ def test_fused_beliefs_identical_to_belief_passes(ctx, capfd, model):
         assert _close(res[0][t], want[t], 1e-5), (t, res[0][t], want[t])
 
 
+@pytest.mark.parametrize("n_parts", [2, 3])
+def test_fused_beliefs_in_tree_parts(ctx, capfd, n_parts):
+    """The segment-owned parts (bnpp_marginals_tree_part, the N-GPU MAR) fuse
+    the beliefs of their own deliveries the same way: every part's marginals
+    bit-identical with and without the fusion, the parts covering every target
+    once, within fp32 rounding of the fp64 per-target engine."""
+    m = bnpp.Model.from_dict(synth.ising_grid(16, 6, seed=35))
+    col = [i * 6 + j for j in range(6) for i in range(16)]
+    want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    got = {}
+    n_fused = 0
+    for kn in ({"BNPP_DUMP_PLAN": "1"}, {"BNPP_NO_BEL_FUSE": "1"}):
+        os.environ.update(kn)
+        os.environ.update({"BNPP_KEEP_LOG2": "8", "BNPP_TREE_SLOTS": "3"})
+        capfd.readouterr()
+        try:
+            parts = [bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F32, order=col, part=p, n_parts=n_parts)[0]
+                     for p in range(n_parts)]
+        finally:
+            for key in list(kn) + ["BNPP_KEEP_LOG2", "BNPP_TREE_SLOTS"]:
+                del os.environ[key]
+        if "BNPP_DUMP_PLAN" in kn:
+            n_fused = sum(" belief: " in ln for ln in capfd.readouterr().err.splitlines())
+        got[tuple(kn)] = parts
+    assert n_fused >= 4, n_fused
+    a, b = got[("BNPP_DUMP_PLAN",)], got[("BNPP_NO_BEL_FUSE",)]
+    assert a == b
+    seen = [t for part in a for t in part]
+    assert sorted(seen) == list(range(m.n_vars))
+    for part in a:
+        for t, p in part.items():
+            assert _close(p, want[t], 1e-5), (t, p, want[t])
+
+
 @pytest.mark.parametrize("keep,slow,rows", [(3, 13, 12), (5, 13, 12), (7, 2, 12), (9, 4, 12), (13, 13, 14)])
 def test_tree_chain_kept_sets_match(ctx, keep, slow, rows):
     """Deliveries from kept sets smaller than the separators (the 32x32 path:
