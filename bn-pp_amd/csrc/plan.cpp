@@ -824,6 +824,11 @@ struct PlanBuilder {
     std::vector<int> rank;
     std::vector<int> level;                 // per table
     bool sequential = false;                // every bucket one level after the previous (program order)
+    // reductions of a delivered kept table (<= 2^24 entries, read once each):
+    // placed one level after their own input, not in program order, so the
+    // reductions at one depth of a delivery's tree share a level and a launch
+    // (the 32x32 MAR made ~3,000 launches of a few microseconds each per call)
+    bool free_small = false;
     int last_level = 0;
     int lane = 0;                           // BucketSpec::lane of the buckets emitted now
 
@@ -873,7 +878,8 @@ struct PlanBuilder {
         b.elim_var = x;
         b.out_vars = ov;
         b.out_table = new_msg(ov);
-        int lv = sequential && !free_level ? last_level : 0;
+        const bool free = free_level || (free_small && table_size(ov, cards) <= ((int64_t)1 << 24));
+        int lv = sequential && !free ? last_level : 0;
         for (const View &v : in) lv = std::max(lv, level[v.table]);
         b.level = lv + 1;
         last_level = std::max(last_level, b.level);
@@ -1721,7 +1727,10 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                     tb = B.emit(bel, slow_j.empty() ? -1 : slow_j[0], false);
                 }
                 if (tb >= 0 && !std::getenv("BNPP_NO_REDUCE_MANY")) {
+                    const char *nf = std::getenv("BNPP_NO_FREE_REDUCE");
+                    B.free_small = !(nf && *nf == '1') && B.p.msgs[tb - B.p.n_src].size <= ((int64_t)1 << 24);
                     B.reduce_many(B.view(tb), mit->second, result_of);
+                    B.free_small = false;
                 } else {
                     for (int t : mit->second)
                         result_of[t] = tb >= 0 ? B.reduce_to({B.view(tb)}, t) : B.reduce_to(bel, t);
