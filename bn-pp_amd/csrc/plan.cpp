@@ -825,10 +825,13 @@ struct PlanBuilder {
     std::vector<int> level;                 // per table
     bool sequential = false;                // every bucket one level after the previous (program order)
     // reductions of a delivered kept table (<= 2^24 entries, read once each):
-    // placed one level after their own input, not in program order, so the
+    // placed one level after their own input (and after free_base, the level
+    // the delivery's reductions start from), not in program order, so the
     // reductions at one depth of a delivery's tree share a level and a launch
-    // (the 32x32 MAR made ~3,000 launches of a few microseconds each per call)
+    // (the 32x32 MAR made ~3,000 launches of a few microseconds each per call);
+    // the next big bucket still follows them all (its arena is unchanged)
     bool free_small = false;
+    int free_base = 0;
     int last_level = 0;
     int lane = 0;                           // BucketSpec::lane of the buckets emitted now
 
@@ -878,8 +881,8 @@ struct PlanBuilder {
         b.elim_var = x;
         b.out_vars = ov;
         b.out_table = new_msg(ov);
-        const bool free = free_level || (free_small && table_size(ov, cards) <= ((int64_t)1 << 24));
-        int lv = sequential && !free ? last_level : 0;
+        const bool small = free_small && table_size(ov, cards) <= ((int64_t)1 << 24);
+        int lv = sequential && !free_level ? (small ? free_base : last_level) : 0;
         for (const View &v : in) lv = std::max(lv, level[v.table]);
         b.level = lv + 1;
         last_level = std::max(last_level, b.level);
@@ -1728,7 +1731,12 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 }
                 if (tb >= 0 && !std::getenv("BNPP_NO_REDUCE_MANY")) {
                     const char *nf = std::getenv("BNPP_NO_FREE_REDUCE");
-                    B.free_small = !(nf && *nf == '1') && B.p.msgs[tb - B.p.n_src].size <= ((int64_t)1 << 24);
+                    // (breadth-first: a depth's tables are live together, so only
+                    // where they are small beside the messages -- a kept table of
+                    // <= 1/64 of the largest -- else the arena would grow)
+                    const int64_t kt = B.p.msgs[tb - B.p.n_src].size;
+                    B.free_small = !(nf && *nf == '1') && kt <= ((int64_t)1 << 24) && kt * 64 <= B.p.max_table;
+                    B.free_base = B.last_level;
                     B.reduce_many(B.view(tb), mit->second, result_of);
                     B.free_small = false;
                 } else {

@@ -172,7 +172,9 @@ def test_bucket_tree_rejects_null_context():
 def test_plan_stats_checkpointed_chain():
     """Column-sweep grids give chain-shaped bucket trees: with few checkpoint
     slots the plan recomputes forward messages (more entries) and runs in
-    program order (one bucket per level)."""
+    program order (one bucket per level), except the reductions of a delivered
+    kept table, which sit one level after their own input and share levels
+    (BNPP_NO_FREE_REDUCE=1: strictly one bucket per level)."""
     import os
     m = bnpp.Model.load(model_path("ising10x10.uai"))
     col = [r * 10 + c for c in range(10) for r in range(10)]
@@ -181,14 +183,17 @@ def test_plan_stats_checkpointed_chain():
     os.environ["BNPP_NO_CHAIN"] = "1"          # one launch per bucket (fused runs add shared G products)
     try:
         ck = bnpp.plan_stats(m, 3, {}, "mf", order=col)
+        os.environ["BNPP_NO_FREE_REDUCE"] = "1"
+        seq = bnpp.plan_stats(m, 3, {}, "mf", order=col)
         with pytest.raises(bnpp.BnppError) as e:     # min-fill on alarm: not a chain
             bnpp.plan_stats(bnpp.Model.load(model_path("alarm.uai")), 3, {}, "mf")
         assert e.value.status == bnpp.ERR_UNSUPPORTED
     finally:
-        del os.environ["BNPP_TREE_SLOTS"]
-        del os.environ["BNPP_NO_CHAIN"]
+        for k in ("BNPP_TREE_SLOTS", "BNPP_NO_CHAIN", "BNPP_NO_FREE_REDUCE"):
+            os.environ.pop(k, None)
     assert ck[0] > full[0]                           # recomputation
-    assert ck[2] == ck[3]                            # one bucket per level
+    assert seq[2] == seq[3]                          # one bucket per level
+    assert ck[2] <= ck[3] and ck[3] == seq[3] and ck[0] == seq[0] and ck[6] == seq[6]
     assert ck[1] < full[1]                           # smaller arena
 
 
