@@ -434,9 +434,13 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             for (int e = 0; e < 16; ++e) lv[e] = gload(lb + (int64_t)slab_e(e) * c.d_slab);
         }
     };
+    // one-run backward launches issue a tile's lam loads before the next
+    // tile's row loads (lam_early): waiting for lam then leaves those in
+    // flight, where loads issued after them drained them
+    bool lam_early = false;
     auto run_tile = [&](float (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
         if constexpr (FORM == kChainBwd && DENSE) {
-            if (c.bel) load_lam(tout);
+            if (c.bel && !lam_early) load_lam(tout);
         }
         if constexpr (FORM == kChainBwd) {
             // rows through the image, then this lane's 16 entries (slots 4.. = w)
@@ -580,10 +584,15 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         // 2^32-entry message, profiles/r04_split_ab.txt)
         decode(vb, in_off, out_off, gb);
         issue(in_off, rg);
+        lam_early = c.bel != nullptr;
         while (true) {
             float t[16];
 #pragma unroll
             for (int e = 0; e < 16; ++e) t[e] = rg[e];
+            if (lam_early) {
+                decode(vb, in_off, out_off, gb);
+                load_lam(tout);
+            }
             const int64_t vbn = vb + gridDim.x;
             decode(vbn < total_vblocks ? vbn : total_vblocks - 1, in_off, out_off, gb);
             issue(in_off, rg);
