@@ -321,6 +321,11 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
+        # an RCCL error or timeout (the sliced leg's first run on RCCL is on the
+        # driver's node) aborts the communicator and raises in the caller --
+        # recorded by sliced_mar -- instead of tearing the process down after
+        # the N-rank record is out (torch's default, mode 3)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
         dist.init_process_group("gloo" if rehearse else "nccl")
     dev = torch.device("cuda", local)
     ctx = bnpp.Context(local)
