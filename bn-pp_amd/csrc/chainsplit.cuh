@@ -421,11 +421,12 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     };
     // kChainBel: the forward message at this lane's 16 output positions of the
     // tile whose rest offset is `to` (the same scattered addresses as the
-    // stores), loaded at the start of the tile so they arrive behind its
-    // exchange.  They are most of a fused run's extra time (10.9 ms per run
-    // against 6.9 ms with the loads removed and 6.3 ms unfused); loading them
-    // a tile ahead was slower still (8.3 ms average over all backward runs
-    // against 7.9 ms, 128 VGPRs) -- profiles/r04_belief_fusion_ab.txt
+    // stores), loaded before the tile's exchange so they arrive behind it --
+    // in one-run launches before the next tile's row prefetch (lam_early,
+    // below).  They are most of a fused run's extra time (10.4 ms per run
+    // against 6.3 ms unfused; 10.9 ms when issued after the prefetch, 6.9 ms
+    // with the loads removed); loading them a whole tile ahead needed 128
+    // VGPRs and was slower -- profiles/r04_belief_fusion_ab.txt
     float lv[16];
     auto load_lam = [&](int64_t to) {
         if constexpr (FORM == kChainBwd && DENSE) {
