@@ -433,3 +433,42 @@ def test_checkpoint_search_picks_a_fitting_slot_count():
             last = st
     finally:
         os.environ.pop("BNPP_MEM_BUDGET_GB", None)
+
+
+def test_plan_fuses_beliefs_and_shares_reduction_levels(capfd):
+    """Host planning of the checkpointed tree (no device): with 2^8-entry kept
+    sets on a 16x6 column sweep, every belief whose summed variables are the
+    slots of the backward run that made its message is formed inside that run
+    (kChainBel: the plan dump marks the run, the separate belief buckets and
+    one read of each message are gone); on a 24x8 sweep with 2^16-entry kept
+    sets (small beside its 2^24-entry messages) the kept tables' reductions
+    share levels (BNPP_NO_FREE_REDUCE restores program order for them) with
+    the same buckets, traffic and arena."""
+    import os
+    from bnpp import synth
+
+    def stats(r, c, env):
+        m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=3))
+        col = [i * c + j for j in range(c) for i in range(r)]
+        os.environ.update(env)
+        capfd.readouterr()
+        try:
+            st = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+        finally:
+            for k in env:
+                del os.environ[k]
+        return st, capfd.readouterr().err
+
+    base = {"BNPP_KEEP_LOG2": "8", "BNPP_TREE_SLOTS": "3", "BNPP_DUMP_PLAN": "1"}
+    fused, err_f = stats(16, 6, base)
+    plain, err_p = stats(16, 6, dict(base, BNPP_NO_BEL_FUSE="1"))
+    n_fused = err_f.count(" belief: ")
+    assert n_fused >= 8 and err_p.count(" belief: ") == 0
+    assert fused[3] == plain[3] - n_fused                # the belief buckets are gone
+    assert fused[6] < plain[6]                           # one read of pi per fused belief
+    assert fused[1] == plain[1]                          # same arena
+    base = {"BNPP_KEEP_LOG2": "16", "BNPP_TREE_SLOTS": "4"}
+    free, _ = stats(24, 8, base)
+    seq, _ = stats(24, 8, dict(base, BNPP_NO_FREE_REDUCE="1"))
+    assert free[2] < seq[2]                              # fewer levels (launches)
+    assert free[3] == seq[3] and free[6] == seq[6] and free[1] == seq[1]
