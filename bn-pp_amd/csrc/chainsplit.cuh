@@ -603,35 +603,38 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             if (vb >= total_vblocks) break;
         }
     } else if constexpr (!MULTI) {
-        // one bucket, forward form: the loads of the next two tiles are in flight while a
-        // tile is computed (register sets A and B alternate: a set is copied
-        // out only once its loads are two tiles old, so no wait exposes
-        // fresh-load latency); loads are issued unconditionally (the last
-        // tile is re-read rather than branching) so the wait counts stay static
-        const int64_t last = total_vblocks - 1, g = gridDim.x;
-        auto clamp = [&](int64_t v) { return v < last ? v : last; };
-        float rb[16];
+        // one bucket, forward form: the next tile's loads go into registers at
+        // the top of a tile and, once the tile is done, into this lane's own
+        // slots of the exchange table, where the next tile reads them back
+        // (its phase 1 then writes its results to those same slots).  The
+        // loop carries no register set with loads in flight: with two
+        // alternating sets the compiled loop copied the freshly loaded set at
+        // the latch, a wait for every load in flight once per two tiles.
+        // Safe without another barrier: a lane reads and rewrites only its own
+        // slots, and it stages the next tile after the tile's image barrier,
+        // which every wave reaches only after its phase-2 reads of the table.
+        // Loads are issued unconditionally (the last tile is re-read rather
+        // than branching) so the wait counts stay static
+        const int64_t last = total_vblocks - 1;
+        float p[16];
+        auto stage = [&]() {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) xch[(w * 16 + e) * 64 + lane] = p[e];
+        };
         decode(vb, in_off, out_off, gb);
-        issue(in_off, rg);
-        decode(clamp(vb + g), in_off, out_off, gb);
-        issue(in_off, rb);
+        issue(in_off, p);
+        stage();
         while (true) {
             float t[16];
 #pragma unroll
-            for (int e = 0; e < 16; ++e) t[e] = rg[e];
-            decode(clamp(vb + 2 * g), in_off, out_off, gb);
-            issue(in_off, rg);
+            for (int e = 0; e < 16; ++e) t[e] = xch[(w * 16 + e) * 64 + lane];
+            const int64_t vbn = vb + gridDim.x;
+            decode(vbn < last ? vbn : last, in_off, out_off, gb);
+            issue(in_off, p);
             decode(vb, in_off, out_off, gb);
             run_tile(t, out_off, gb);
-            vb += g;
-            if (vb >= total_vblocks) break;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) t[e] = rb[e];
-            decode(clamp(vb + 2 * g), in_off, out_off, gb);
-            issue(in_off, rb);
-            decode(vb, in_off, out_off, gb);
-            run_tile(t, out_off, gb);
-            vb += g;
+            stage();
+            vb = vbn;
             if (vb >= total_vblocks) break;
         }
     } else {
