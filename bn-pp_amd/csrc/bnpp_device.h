@@ -88,7 +88,15 @@ struct BucketDesc {
     int32_t lanes;
     // kChainBel: the belief table the run also writes
     int32_t aux_out;
+    // slab form with outer dims (outer_n > 0 combinations of the output dims
+    // slower than the slab dim, each a run of whole virtual blocks):
+    // outer_div = (dim header, magic) of the blocks per combination; the pool
+    // at dim_off + outer_rel holds, per combination, n_in offsets added to the
+    // inputs' bases (the big input's net of the combination's output offset)
+    int32_t outer_n, outer_rel;
+    int64_t outer_div[2];
 };
+constexpr int kSlabMaxOuter = 64;
 
 // arguments of one level launch (a group of buckets of one kernel variant)
 struct LevelArgs {

@@ -128,7 +128,7 @@ int run_single(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &c
     std::memset(&a, 0, sizeof a);
     std::vector<int64_t> pool;
     std::string msg;
-    if (!build_desc(b, cards, max_vec_for(dtype), a.d, pool, &msg)) return set_err(BNPP_ERR_INVALID, msg);
+    if (!build_desc(b, cards, max_vec_for(dtype), a.d, pool, &msg, false)) return set_err(BNPP_ERR_INVALID, msg);
     if (pool.size() > (size_t)kMaxPool)
         return set_err(BNPP_ERR_UNSUPPORTED, "too many non-mergeable output dims for a single-op call");
     std::copy(pool.begin(), pool.end(), a.pool);

@@ -496,7 +496,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
 }
 
 bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec, BucketDesc &d,
-                std::vector<int64_t> &pool, std::string *msg) {
+                std::vector<int64_t> &pool, std::string *msg, bool slab_outer) {
     if (!b.chain_x.empty()) return build_chain_desc(b, cards, max_vec, d, pool, msg);
     const int n = (int)b.in.size();
     if (n < 1 || n > kMaxIn) {
@@ -555,6 +555,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         return false;
     }
     std::vector<int64_t> out_strides;     // kOutStrided: output stride per (permuted) dim
+    std::vector<int64_t> outer_tab;       // slab form, outer dims: base offsets per combination and input
     int k = 1;
     int64_t es[kMaxIn] = {0};
     if (b.elim_var >= 0) {
@@ -639,16 +640,34 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
             int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
             int64_t s1 = merged.size() < 2 ? 0 : merged[1].s[big];
             // slab form (slab.cuh): the big input is k slabs contiguous along the
-            // output's slow dim (its only other dim, of card 1/2/4, it does not
-            // vary along), every small input is constant along that slow dim
-            int slab_v = 0, slab_c0 = 1;
+            // output's slab dim (dim 0, or dim 1 after a dim of card 2/4 it does
+            // not vary along), every small input is constant along the slab dim.
+            // Output dims slower than the slab dim ("outer", level launches only)
+            // are enumerated as whole runs of virtual blocks: per combination the
+            // inputs' bases move (a column sweep's first buckets multiply a
+            // message by factors over new variables: [2^30 slab][2][2])
+            int slab_v = 0, slab_c0 = 1, slab_dim = -1;
+            int64_t slab_outer_n = 1;
             {
                 const char *ns = std::getenv("BNPP_NO_SLAB");
-                const bool two = merged.size() == 2;
-                const Dim *sd = two ? &merged[1] : merged.size() == 1 ? &merged[0] : nullptr;
-                slab_c0 = two ? (int)merged[0].card : 1;
-                bool ok = !(ns && *ns == '1') && sd && k >= 1 && k <= 4 && sd->s[big] == 1 &&
-                          (!two || merged[0].s[big] == 0) && (slab_c0 == 1 || slab_c0 == 2 || slab_c0 == 4);
+                const char *no = std::getenv("BNPP_NO_SLAB_OUTER");
+                if (!merged.empty() && merged[0].s[big] == 1) slab_dim = 0;
+                else if (merged.size() >= 2 && merged[0].s[big] == 0 && merged[1].s[big] == 1) slab_dim = 1;
+                if (slab_dim >= 0)
+                    for (size_t j = (size_t)slab_dim + 1; j < merged.size(); ++j)
+                        slab_outer_n = sat_mul(slab_outer_n, (int64_t)merged[j].card);
+                // outer dims only with the slab dim fastest (C0 = 1): measured on the
+                // 32x32 sweep, [2 y][2^30 slab][2] k=2 buckets ran 3.8 TB/s as slab
+                // tiles (C0 = 2, V = 2 or 4) against 4.2 for the stream kernel, while
+                // [2^30 slab][2][2] k=1 went 1.7 -> 5.4 TB/s (profiles/r04_slab_outer_ab.txt)
+                const char *oc = std::getenv("BNPP_SLAB_OUTER_MAXC0");      // A/B knob
+                const int64_t max_c0 = oc ? std::atoll(oc) : 1;
+                if (slab_outer_n > 1 && (!slab_outer || (no && *no == '1') || slab_outer_n > kSlabMaxOuter ||
+                                         (slab_dim == 1 && (int64_t)merged[0].card > max_c0)))
+                    slab_dim = -1;
+                const Dim *sd = slab_dim >= 0 ? &merged[slab_dim] : nullptr;
+                slab_c0 = slab_dim == 1 ? (int)merged[0].card : 1;
+                bool ok = !(ns && *ns == '1') && sd && k >= 1 && k <= 4 && (slab_c0 == 1 || slab_c0 == 2 || slab_c0 == 4);
                 for (int i = 0; ok && i < n; ++i)
                     if (i != big && sd->s[i] != 0) ok = false;
                 if (ok) {
@@ -662,6 +681,17 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                         if (inst) vn = want;
                     }
                     if ((int64_t)sd->card % vn || b.in[big].base % vn || es[big] % vn) vn = 1;
+                    for (size_t j = (size_t)slab_dim + 1; j < merged.size(); ++j)
+                        if (merged[j].s[big] % vn) vn = 1;
+                    if (slab_outer_n > 1) {
+                        // every combination's tiles fill whole virtual blocks
+                        auto fits = [&](int v) {
+                            const char *sl = std::getenv("BNPP_SLAB_LANES");
+                            const int lanes = slab_c0 * v * eb == 32 && !(sl && *sl == '1') ? 2 : 1;
+                            return ((int64_t)sd->card / v) % (kBlock / lanes) == 0;
+                        };
+                        if (!fits(vn)) vn = fits(1) ? 1 : 0;
+                    }
                     slab_v = vn;
                 }
             }
@@ -681,6 +711,26 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     d.in_lds_off[i] = 0;
                 }
                 d.small_elems = 0;
+                if (slab_outer_n > 1) {
+                    const int64_t S = (int64_t)merged[slab_dim].card;
+                    const int64_t per_vb = kBlock / d.lanes;
+                    uint32_t shift, magic;
+                    bool pow2;
+                    magic_for((uint32_t)(S / v2 / per_vb), shift, magic, pow2);
+                    d.outer_n = (int32_t)slab_outer_n;
+                    d.outer_div[0] = pack_dim_header((uint32_t)(S / v2 / per_vb), shift, pow2);
+                    d.outer_div[1] = (int64_t)magic;
+                    outer_tab.resize((size_t)(slab_outer_n * n));
+                    for (int64_t o = 0; o < slab_outer_n; ++o) {
+                        int64_t rem = o;
+                        for (int i = 0; i < n; ++i) outer_tab[o * n + i] = i == big ? -o * S : 0;
+                        for (size_t j = (size_t)slab_dim + 1; j < merged.size(); ++j) {
+                            const int64_t x = rem % (int64_t)merged[j].card;
+                            rem /= (int64_t)merged[j].card;
+                            for (int i = 0; i < n; ++i) outer_tab[o * n + i] += x * merged[j].s[i];
+                        }
+                    }
+                }
             } else {
             // optional narrow tile: when the big input is constant along the
             // fastest output dim and v1 entries already fill a 16-B store, drop
@@ -795,6 +845,10 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
     }
     if (d.flags & kOutStrided)
         for (int64_t o : out_strides) pool.push_back(o);
+    if (d.outer_n > 0) {
+        d.outer_rel = (int32_t)((int64_t)pool.size() - d.dim_off);
+        pool.insert(pool.end(), outer_tab.begin(), outer_tab.end());
+    }
     return true;
 }
 
@@ -2485,7 +2539,9 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 for (int q = 0; q < d.n_in; ++q) std::fprintf(stderr, "%s%lld", q ? "," : "", (long long)d.elim_stride[q]);
                 std::fprintf(stderr, " tables:");
                 for (int q = 0; q < d.n_in; ++q) std::fprintf(stderr, "%s%d", q ? "," : "", d.in_table[q]);
-                std::fprintf(stderr, "->%d\n", d.out_table);
+                std::fprintf(stderr, "->%d", d.out_table);
+                if (d.outer_n > 0) std::fprintf(stderr, " outer=%d", d.outer_n);
+                std::fprintf(stderr, "\n");
             }
         }
         g.end = (int)i;

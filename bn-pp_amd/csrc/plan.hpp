@@ -104,7 +104,7 @@ constexpr int kXchgKeyBase = 1 << 24;
 // Compile one bucket into a descriptor + dims-pool rows.  max_vec: 4 (fp32) / 2 (fp64).
 // Returns false (with msg) on an invalid shape.
 bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec, BucketDesc &d,
-                std::vector<int64_t> &pool, std::string *msg);
+                std::vector<int64_t> &pool, std::string *msg, bool slab_outer = true);
 
 // Fused chain runs: is the chain kernel with this key (bnpp_device.h,
 // chain_key) instantiated for this element size (k_chain_f32/f64.hip)?

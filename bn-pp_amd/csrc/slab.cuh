@@ -91,9 +91,9 @@ struct SlabTile {
     }
 };
 
-// stride of small input i along y (output dim 0 when the output has 2 dims)
+// stride of small input i along y (output dim 0 when C0 = v1 > 1)
 __device__ __forceinline__ int64_t slab_sy(const BucketDesc &d, const int64_t *dims, int i) {
-    return d.n_dims == 2 ? dims[2 + i] : 0;
+    return d.v1 > 1 ? dims[2 + i] : 0;
 }
 
 template <typename T, int K, int C0, int V, bool NTL>
@@ -158,9 +158,17 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
     const int big = d.big;
     const int64_t t = (vb - d.vblk_begin) * (kBlock / H) + threadIdx.x / H;     // H lanes per tile
     const bool live = t < d.n_tiles;
+    // outer dims: this block's combination (uniform) moves every input's base
+    const int64_t *adj = nullptr;
+    if (d.outer_n > 0) {
+        uint64_t q, r;
+        divmod_dim((uint64_t)(vb - d.vblk_begin), d.outer_div[0], d.outer_div[1], q, r);
+        adj = dims + d.outer_rel + (int64_t)q * d.n_in;
+    }
+    auto base_of = [&](int i) { return adj ? d.in_base[i] + adj[i] : d.in_base[i]; };
     T m[K][V];
     if (live)
-        slab_load_big<T, K, C0, V, kNtLoad>(static_cast<const T *>(meta[d.in_table[big]].ptr) + d.in_base[big] + t * V,
+        slab_load_big<T, K, C0, V, kNtLoad>(static_cast<const T *>(meta[d.in_table[big]].ptr) + base_of(big) + t * V,
                                             d.elim_stride[big], m);
     int64_t e_sum = 0, x_sum = 0;
 #pragma unroll
@@ -180,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
     if (live) {
         T acc[ST::N];
         ST::compute(m, big, d.n_in, [&](int i, T (&g)[K][C0]) {
-            ST::load_small(static_cast<const T *>(meta[d.in_table[i]].ptr) + d.in_base[i], d.elim_stride[i],
+            ST::load_small(static_cast<const T *>(meta[d.in_table[i]].ptr) + base_of(i), d.elim_stride[i],
                            slab_sy(d, dims, i), g);
         }, acc);
         if (d.flags & kScale) {

@@ -421,6 +421,42 @@ def test_split_runs_peaked_potentials(ctx, capfd, rows, cols, log2_eps):
         assert _close(res[0][1][t], want[t], 1e-5), (t, res[0][1][t], want[t])
 
 
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_slab_outer_dims_identical_to_stream(ctx, capfd, dt):
+    """A column sweep's first buckets multiply a growing message by factors
+    over new variables: [S slab][2][2] outputs whose big input is contiguous
+    along the slab dim and constant or strided along the slower ones.  They run
+    as slab tiles with the slower dims enumerated per block (outer=4), bit-
+    identical to the stream kernel (BNPP_NO_SLAB_OUTER) and to one bucket per
+    launch without either (BNPP_NO_SLAB + BNPP_NO_CHAIN): same product order
+    (factor.cpp:131-143), same rescale.  fp64 tree marginals also match the
+    per-target engine to 1e-12."""
+    r = c = 16
+    m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=41))
+    col = [i * c + j for j in range(c) for i in range(r)]
+    d = bnpp.F64 if dt == "f64" else bnpp.F32
+    knobs = [{"BNPP_DUMP_PLAN": "1"}, {"BNPP_NO_SLAB_OUTER": "1"}, {"BNPP_NO_SLAB": "1", "BNPP_NO_CHAIN": "1"}]
+    res = []
+    for kn in knobs:
+        os.environ.update(kn)
+        capfd.readouterr()
+        try:
+            res.append([bnpp.partition(ctx, m, {}, "mf", d, order=col)[0],
+                        bnpp.marginals_tree(ctx, m, {}, "mf", d, order=col)[0]])
+        finally:
+            for key in kn:
+                del os.environ[key]
+        if "BNPP_DUMP_PLAN" in kn:
+            outer = [ln for ln in capfd.readouterr().err.splitlines() if " outer=" in ln]
+            assert len(outer) >= 2, len(outer)
+    for out in res[1:]:
+        assert out == res[0]
+    if dt == "f64":
+        want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+        for t in range(m.n_vars):
+            assert _close(res[0][1][t], want[t], 1e-12), (t, res[0][1][t], want[t])
+
+
 def _two_grids(a, b):
     n = len(a["cards"])
     return {"type": "MARKOV", "cards": a["cards"] + b["cards"],

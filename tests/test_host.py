@@ -472,3 +472,33 @@ def test_plan_fuses_beliefs_and_shares_reduction_levels(capfd):
     seq, _ = stats(24, 8, dict(base, BNPP_NO_FREE_REDUCE="1"))
     assert free[2] < seq[2]                              # fewer levels (launches)
     assert free[3] == seq[3] and free[6] == seq[6] and free[1] == seq[1]
+
+
+def test_plan_slab_outer_dims(capfd):
+    """Host planning (no device): a 16x16 column sweep's first-column buckets
+    ([S slab][2][2], k = 1, the big input contiguous along S) take the slab form
+    with the slower dims enumerated per block (plan dump `outer=4`, slab class
+    8); BNPP_NO_SLAB_OUTER sends them back to the stream kernel with the same
+    buckets, traffic and arena."""
+    import os
+    from bnpp import synth
+
+    m = bnpp.Model.from_dict(synth.ising_grid(16, 16, seed=3))
+    col = [i * 16 + j for j in range(16) for i in range(16)]
+
+    def stats(env):
+        os.environ.update(env)
+        capfd.readouterr()
+        try:
+            st = bnpp.plan_stats(m, 3, {}, "mf", dtype=bnpp.F32, order=col)
+        finally:
+            for k in env:
+                del os.environ[k]
+        return st, capfd.readouterr().err
+
+    on, err_on = stats({"BNPP_DUMP_PLAN": "1"})
+    off, err_off = stats({"BNPP_DUMP_PLAN": "1", "BNPP_NO_SLAB_OUTER": "1"})
+    outer = [ln for ln in err_on.splitlines() if " outer=" in ln]
+    assert len(outer) >= 2 and all("bcls=8" in ln for ln in outer) and any("k=1" in ln for ln in outer), outer
+    assert " outer=" not in err_off
+    assert on[3] == off[3] and on[6] == off[6] and on[1] == off[1]
