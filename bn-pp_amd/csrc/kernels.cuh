@@ -678,7 +678,11 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
         }
     } else {
 #ifndef BNPP_STREAM_U
-#define BNPP_STREAM_U 16     // measured: forward 2x8 Col 4.78 -> 5.49 TB/s, others unchanged
+// measured: 16 -> forward 2x8 Col 4.78 -> 5.49 TB/s; 32 -> the 32x32 sweep's
+// k = 2 2x8 full tiles (two 64-B loads in flight instead of one) 13.1 -> 9.7 ms
+// per 2^32-entry output, MAR stream time 186 -> 172 ms per two calls
+// (profiles/r04_stream_u_ab.txt; 64 spills back to 13.1 ms)
+#define BNPP_STREAM_U 32
 #endif
         // values of the summed variable whose big loads are issued together;
         // BNPP_STREAM_U > 0 caps the registers they take at that many entries
