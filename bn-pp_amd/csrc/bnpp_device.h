@@ -95,6 +95,8 @@ struct BucketDesc {
     // inputs' bases (the big input's net of the combination's output offset)
     int32_t outer_n, outer_rel;
     int64_t outer_div[2];
+    // slab level launches: passes of kBlock / lanes tiles per block (0/1, or 2)
+    int32_t slab_r;
 };
 constexpr int kSlabMaxOuter = 64;
 
@@ -123,7 +125,10 @@ __host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return ni
 // stream kernels: 4096 + big-class * 256 + v1 * 16 + v2  (v1, v2 <= 8)
 __host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 256 + v1 * 16 + v2; }
 // slab kernels (slab.cuh): K summed values, C0 entries of output dim 0, V slow-dim entries per lane
-__host__ __device__ constexpr int slab_key(int k, int c0, int v, int h = 1) { return 16384 + k * 256 + c0 * 16 + v + (h == 2 ? 8 : 0); }
+// and R passes of tiles per block (level launches, BucketDesc::slab_r: 1 or 2)
+__host__ __device__ constexpr int slab_key(int k, int c0, int v, int h = 1, int r = 1) {
+    return 16384 + k * 1024 + (r == 4 ? 512 : r == 2 ? 256 : 0) + c0 * 16 + v + (h == 2 ? 8 : 0);
+}
 
 // Chain (sweep) form: F consecutive buckets of an elimination chain in one
 // pass.  Input 0 is the message entering the run; bucket j of the run sums

@@ -8,7 +8,7 @@ hipError_t dispatch_slab_single_f64(int key, const SingleArgs &a, hipStream_t st
     return hipErrorInvalidValue;
 }
 hipError_t dispatch_slab_level_f64(int key, const LevelArgs &a, hipStream_t stream) {
-    switch (key) { BNPP_SLAB_F64(BNPP_CASE_SLAB_LEVEL, double) default: break; }
+    switch (key) { BNPP_SLAB_F64(BNPP_CASE_SLAB_LEVEL, double) BNPP_SLAB_R2_F64(BNPP_CASE_SLAB_LEVEL_R2, double) default: break; }
     return hipErrorInvalidValue;
 }
 }  // namespace bnpp

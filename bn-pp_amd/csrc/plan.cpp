@@ -656,12 +656,13 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 if (slab_dim >= 0)
                     for (size_t j = (size_t)slab_dim + 1; j < merged.size(); ++j)
                         slab_outer_n = sat_mul(slab_outer_n, (int64_t)merged[j].card);
-                // outer dims only with the slab dim fastest (C0 = 1): measured on the
-                // 32x32 sweep, [2 y][2^30 slab][2] k=2 buckets ran 3.8 TB/s as slab
-                // tiles (C0 = 2, V = 2 or 4) against 4.2 for the stream kernel, while
-                // [2^30 slab][2][2] k=1 went 1.7 -> 5.4 TB/s (profiles/r04_slab_outer_ab.txt)
+                // outer dims with C0 <= 2: measured on the 32x32 sweep, [2^30 slab][2][2]
+                // k=1 buckets went 1.7 -> 5.4 TB/s (6.1 with two passes per block),
+                // [2 y][2^30 slab][2] k=2 ones ran 3.8 TB/s as one-pass slab tiles against
+                // 4.2 for the stream kernel, 4.5 with two passes (profiles/r04_slab_outer_ab.txt,
+                // r04_slab_passes_ab.txt)
                 const char *oc = std::getenv("BNPP_SLAB_OUTER_MAXC0");      // A/B knob
-                const int64_t max_c0 = oc ? std::atoll(oc) : 1;
+                const int64_t max_c0 = oc ? std::atoll(oc) : 2;
                 if (slab_outer_n > 1 && (!slab_outer || (no && *no == '1') || slab_outer_n > kSlabMaxOuter ||
                                          (slab_dim == 1 && (int64_t)merged[0].card > max_c0)))
                     slab_dim = -1;
@@ -690,6 +691,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                             const int lanes = slab_c0 * v * eb == 32 && !(sl && *sl == '1') ? 2 : 1;
                             return ((int64_t)sd->card / v) % (kBlock / lanes) == 0;
                         };
+                        // (two passes per block need twice that: checked below)
                         if (!fits(vn)) vn = fits(1) ? 1 : 0;
                     }
                     slab_v = vn;
@@ -711,9 +713,20 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     d.in_lds_off[i] = 0;
                 }
                 d.small_elems = 0;
+                // level launches: two passes of tiles per block, both passes' loads
+                // issued first (instantiated: f32 (C0, V) = (1, 4), (2, 2); f64 (1, 2); H = 1)
+                d.slab_r = 1;
+                {
+                    const char *sr = std::getenv("BNPP_SLAB_R");          // A/B knob: 1 = one pass
+                    const bool inst = d.lanes == 1 && ((eb == 4 && ((v1 == 1 && v2 == 4) || (v1 == 2 && v2 == 2))) ||
+                                                       (eb == 8 && v1 == 1 && v2 == 2));
+                    if (slab_outer && !(sr && std::atoi(sr) == 1) && inst &&
+                        (slab_outer_n == 1 || ((int64_t)merged[slab_dim].card / v2) % (2 * kBlock) == 0))
+                        d.slab_r = 2;
+                }
                 if (slab_outer_n > 1) {
                     const int64_t S = (int64_t)merged[slab_dim].card;
-                    const int64_t per_vb = kBlock / d.lanes;
+                    const int64_t per_vb = kBlock / d.lanes * d.slab_r;
                     uint32_t shift, magic;
                     bool pow2;
                     magic_for((uint32_t)(S / v2 / per_vb), shift, magic, pow2);
@@ -2459,7 +2472,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
         it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf)
-                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes)
+                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes, it.d.slab_r)
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2)
                  : b.simple ? variant_key(kMaxIn, 1, 1)         // the widest input class runs any input count
                             : variant_key(it.d.n_in, it.d.v1, it.d.v2);
@@ -2502,7 +2515,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
             BucketDesc &d = s.descs[i];
             d.vblk_begin = vb;
             const int64_t per_vb = d.chain && chain_split_form((d.chain >> 16) & 0xf) ? kSplitRowsHost
-                                   : d.big >= 0 && d.bcls == kBigSlab && d.lanes == 2 ? kBlock / 2 : kBlock;
+                                   : d.big >= 0 && d.bcls == kBigSlab ? kBlock / (d.lanes == 2 ? 2 : 1) * std::max(1, d.slab_r)
+                                                                          : kBlock;
             vb += (d.n_tiles + per_vb - 1) / per_vb;
             g.small_elems = std::max(g.small_elems, d.big >= 0 || d.chain ? d.small_elems : 0);
             if (dump && d.chain) {
@@ -2541,6 +2555,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 for (int q = 0; q < d.n_in; ++q) std::fprintf(stderr, "%s%d", q ? "," : "", d.in_table[q]);
                 std::fprintf(stderr, "->%d", d.out_table);
                 if (d.outer_n > 0) std::fprintf(stderr, " outer=%d", d.outer_n);
+                if (d.slab_r > 1) std::fprintf(stderr, " passes=%d", d.slab_r);
                 std::fprintf(stderr, "\n");
             }
         }

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs ar
 // Level form: one workgroup per virtual block of a level's slab buckets (flat
 // grid), with the VE rescaling (kScale) and the max tracking (kTrackMax) of
 // the other level kernels.
-template <typename T, int K, int C0, int V, int H>
+template <typename T, int K, int C0, int V, int H, int R>
 __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                             const int64_t *__restrict__ pool,
                                                             TableMeta *__restrict__ meta) {
@@ -156,8 +156,10 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
     const BucketDesc &d = descs[bi];
     const int64_t *dims = pool + d.dim_off;
     const int big = d.big;
-    const int64_t t = (vb - d.vblk_begin) * (kBlock / H) + threadIdx.x / H;     // H lanes per tile
-    const bool live = t < d.n_tiles;
+    // H lanes per tile; R passes of kBlock / H tiles per block, every pass's
+    // loads issued before the first tile is computed
+    constexpr int TPP = kBlock / H;
+    const int64_t t0 = (vb - d.vblk_begin) * (TPP * R) + threadIdx.x / H;
     // outer dims: this block's combination (uniform) moves every input's base
     const int64_t *adj = nullptr;
     if (d.outer_n > 0) {
@@ -166,10 +168,13 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
         adj = dims + d.outer_rel + (int64_t)q * d.n_in;
     }
     auto base_of = [&](int i) { return adj ? d.in_base[i] + adj[i] : d.in_base[i]; };
-    T m[K][V];
-    if (live)
-        slab_load_big<T, K, C0, V, kNtLoad>(static_cast<const T *>(meta[d.in_table[big]].ptr) + base_of(big) + t * V,
-                                            d.elim_stride[big], m);
+    T m[R][K][V];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (t0 + r * TPP < d.n_tiles)
+            slab_load_big<T, K, C0, V, kNtLoad>(static_cast<const T *>(meta[d.in_table[big]].ptr) + base_of(big) +
+                                                    (t0 + r * TPP) * V,
+                                                d.elim_stride[big], m[r]);
     int64_t e_sum = 0, x_sum = 0;
 #pragma unroll
     for (int i = 0; i < kSlabMaxIn; ++i) {
@@ -185,9 +190,12 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
     }
     if (vb == d.vblk_begin && threadIdx.x == 0) meta[d.out_table].exp2 = x_sum;
     T lmax = T(0);
-    if (live) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t t = t0 + r * TPP;
+        if (t >= d.n_tiles) break;
         T acc[ST::N];
-        ST::compute(m, big, d.n_in, [&](int i, T (&g)[K][C0]) {
+        ST::compute(m[r], big, d.n_in, [&](int i, T (&g)[K][C0]) {
             ST::load_small(static_cast<const T *>(meta[d.in_table[i]].ptr) + base_of(i), d.elim_stride[i],
                            slab_sy(d, dims, i), g);
         }, acc);
@@ -226,9 +234,9 @@ static hipError_t go_slab_single(const SingleArgs &a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <typename T, int K, int C0, int V, int H>
+template <typename T, int K, int C0, int V, int H, int R>
 static hipError_t go_slab_level(const LevelArgs &a, hipStream_t stream) {
-    hipLaunchKernelGGL((slab_level_kernel<T, K, C0, V, H>), dim3((unsigned)a.vblocks), dim3(kBlock), 0, stream, a.descs,
+    hipLaunchKernelGGL((slab_level_kernel<T, K, C0, V, H, R>), dim3((unsigned)a.vblocks), dim3(kBlock), 0, stream, a.descs,
                        a.n_desc, a.pool, a.meta);
     return hipGetLastError();
 }
@@ -245,6 +253,12 @@ static hipError_t go_slab_level(const LevelArgs &a, hipStream_t stream) {
 #define BNPP_CASE_SLAB_SINGLE(T, K, C0, V, H) \
     case slab_key(K, C0, V, H): return go_slab_single<T, K, C0, V, H>(a, stream);
 #define BNPP_CASE_SLAB_LEVEL(T, K, C0, V, H) \
-    case slab_key(K, C0, V, H): return go_slab_level<T, K, C0, V, H>(a, stream);
+    case slab_key(K, C0, V, H): return go_slab_level<T, K, C0, V, H, 1>(a, stream);
+// level launches with two passes per block (BucketDesc::slab_r; four measured
+// slower, profiles/r04_slab_passes_ab.txt)
+#define BNPP_SLAB_R2_F32(X, T) BNPP_SLAB_K(X, T, 1, 4, 1) BNPP_SLAB_K(X, T, 2, 2, 1)
+#define BNPP_SLAB_R2_F64(X, T) BNPP_SLAB_K(X, T, 1, 2, 1)
+#define BNPP_CASE_SLAB_LEVEL_R2(T, K, C0, V, H) \
+    case slab_key(K, C0, V, H, 2): return go_slab_level<T, K, C0, V, H, 2>(a, stream);
 
 }  // namespace bnpp

@@ -6,11 +6,11 @@ set -o pipefail
 R=$PWD
 export TMPDIR=/tmp
 for e in "$@"; do
-  tag=$(echo "$e" | tr '=' '_')
+  tag=$(echo "$e" | tr '= ' '_+')
   OUT=$R/gpurun_out/slabo/$tag
   mkdir -p $OUT
   if [ "$e" = "-" ]; then e="BNPP_AB_NONE=1"; fi
-  (cd /tmp && export $e && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o k --output-format csv -- python3 $R/tools/mar_grid.py --rows 32 --cols 32 --check 1 --reps 2 > $OUT/log 2>&1) || { tail -5 $OUT/log; exit 1; }
+  (cd /tmp && for kv in $e; do export $kv; done && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o k --output-format csv -- python3 $R/tools/mar_grid.py --rows 32 --cols 32 --check 1 --reps 2 > $OUT/log 2>&1) || { tail -5 $OUT/log; exit 1; }
   echo "== $e"; grep -E '"mar"|"check"' $OUT/log | cut -c1-160
   python3 - $OUT/k_kernel_stats.csv <<'PY'
 import csv, re, sys
