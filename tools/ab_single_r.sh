@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the BNPP_SLAB_SINGLE_R variant was measured and removed: profiles/r04_single_passes_ab.txt)
 # Bench bucket (single-op slab kernel, f32 and the fp64 leg): one pass vs two
 # passes of tiles per block (BNPP_SLAB_SINGLE_R=2), interleaved, 3 rounds.
 set -o pipefail
