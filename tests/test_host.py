@@ -478,8 +478,8 @@ def test_plan_slab_outer_dims(capfd):
     """Host planning (no device): a 16x16 column sweep's first-column buckets
     ([S slab][2][2], k = 1, the big input contiguous along S) take the slab form
     with the slower dims enumerated per block (plan dump `outer=4`, slab class
-    8); BNPP_NO_SLAB_OUTER sends them back to the stream kernel with the same
-    buckets, traffic and arena."""
+    8, two passes of tiles per block); BNPP_NO_SLAB_OUTER sends them back to
+    the stream kernel with the same buckets, traffic and arena."""
     import os
     from bnpp import synth
 
@@ -500,5 +500,6 @@ def test_plan_slab_outer_dims(capfd):
     off, err_off = stats({"BNPP_DUMP_PLAN": "1", "BNPP_NO_SLAB_OUTER": "1"})
     outer = [ln for ln in err_on.splitlines() if " outer=" in ln]
     assert len(outer) >= 2 and all("bcls=8" in ln for ln in outer) and any("k=1" in ln for ln in outer), outer
+    assert any(" passes=2" in ln for ln in outer), outer          # level slab blocks: two passes of tiles
     assert " outer=" not in err_off
     assert on[3] == off[3] and on[6] == off[6] and on[1] == off[1]
