@@ -724,9 +724,11 @@ uint64_t call_key(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, c
     auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
     mix(m->uid);
     mix((uint64_t)kind);
-    std::vector<int> ev(m->d.cards.size(), -1);            // evidence as a per-variable array
-    for (int i = 0; i < n_ev; ++i)
-        if (ev_vars && ev_vals && ev_vars[i] >= 0 && ev_vars[i] < (int)ev.size()) ev[ev_vars[i]] = ev_vals[i];
+    // evidence as a per-variable array; invalid evidence is never cached, so the
+    // call goes on to create_job and fails there with BNPP_ERR_INVALID
+    std::vector<int> ev;
+    std::string msg;
+    if (!evidence_array(m->d, n_ev, ev_vars, ev_vals, ev, msg)) return 0;
     for (int x : ev) mix((uint32_t)x);
     mix((uint64_t)heuristic);
     mix((uint64_t)n_order);

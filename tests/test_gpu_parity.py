@@ -610,3 +610,24 @@ def test_job_cache_reuses_only_identical_calls(ctx):
     want, _ = rm.marginals({}, "mf")
     for t in range(m.n_vars):
         assert all(abs(a - b) <= 1e-12 for a, b in zip(mg[t], want[t]))
+
+
+def test_job_cache_never_serves_invalid_evidence(ctx):
+    """A valid one-shot call leaves its job cached; a following call with
+    out-of-range evidence (a variable past the model, a negative or too large
+    value) must fail with BNPP_ERR_INVALID, not relaunch the cached job
+    (capi.cpp call_key validates the evidence like evidence_array)."""
+    from bnpp import synth
+    d = synth.ising_grid(4, 5, seed=3)
+    m = bnpp.Model.from_dict(d)
+    for kind in ("pr", "mar", "tree"):
+        call = {"pr": lambda ev: bnpp.partition(ctx, m, ev, "mf", bnpp.F64),
+                "mar": lambda ev: bnpp.marginals(ctx, m, ev, "mf", bnpp.F64),
+                "tree": lambda ev: bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F64)}[kind]
+        call({})
+        call({})
+        assert bnpp.last_timing()["plan_ms"] == 0.0        # cached
+        for bad in ({999: 0}, {2: -1}, {2: 2}):
+            with pytest.raises(bnpp.BnppError):
+                call(bad)
+        call({})
