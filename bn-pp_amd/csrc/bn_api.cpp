@@ -74,21 +74,16 @@ double seq_sum(const std::vector<double> &v) {
     return p;
 }
 
-// an output table plus one trailing double for the op's partition sum
-// (bnpp.h out_sum), downloaded together
+// an output table of n doubles
 struct OutBuf : DevBuf {
     uint64_t n;
-    explicit OutBuf(uint64_t n_) : DevBuf((std::max<uint64_t>(n_, 1) + 1) * sizeof(double)), n(n_) {}
-    double *sum() const { return static_cast<double *>(p) + std::max<uint64_t>(n, 1); }
+    explicit OutBuf(uint64_t n_) : DevBuf(std::max<uint64_t>(n_, 1) * sizeof(double)), n(n_) {}
 };
 
-// the table and the reference's running sum (Factor::_partition) computed
-// on the device in the reference's order (factor.cpp:139, 172, 208, 236)
-std::vector<double> download(const OutBuf &b, double &partition) {
-    std::vector<double> v(std::max<uint64_t>(b.n, 1) + 1);
+std::vector<double> download(const OutBuf &b) {
+    std::vector<double> v(std::max<uint64_t>(b.n, 1));
     check(bnpp_synchronize(ctx(), nullptr), "synchronize");
     check(bnpp_memcpy_d2h(ctx(), v.data(), b.p, v.size() * sizeof(double)), "memcpy d2h");
-    partition = v.back();
     v.resize(b.n);
     return v;
 }
@@ -178,13 +173,25 @@ std::ostream &operator<<(std::ostream &o, const Domain &d) {
 }
 
 // ----------------------------------------------------------------- Factor
+// A pending partition sum: `in` null -- the factor's own values in linear
+// order (product / divide / conditioning: factor.cpp:129-139, 161-172,
+// 226-236); otherwise sum_out's terms, the input's entries in (output entry,
+// summed value) order (factor.cpp:196-208): the input seen as [hi][k][lo]
+// (lo = the summed variable's stride), entry i = h * lo + l adds in[h][0..k)[l].
+struct Factor::PendingSum {
+    std::shared_ptr<const std::vector<double>> in;
+    uint64_t k = 1, lo = 1;
+};
+
 Factor::Factor(const Domain *domain, std::vector<double> values, double partition)
     : _domain(domain), _values(std::move(values)), _partition(partition) {}
 Factor::Factor(const Domain *domain, double value)
     : _domain(domain), _values(domain->size(), value), _partition(domain->size() * value) {}
 Factor::Factor(double value) : _domain(new Domain()), _values(1, value), _partition(value) {}
-Factor::Factor(const Factor &f) : _domain(new Domain(*f._domain)), _values(f._values), _partition(f._partition) {}
-Factor::Factor(Factor &&f) noexcept : _domain(f._domain), _values(std::move(f._values)), _partition(f._partition) {
+Factor::Factor(const Factor &f)
+    : _domain(new Domain(*f._domain)), _values(f._values), _partition(f._partition), _pending(f._pending) {}
+Factor::Factor(Factor &&f) noexcept
+    : _domain(f._domain), _values(std::move(f._values)), _partition(f._partition), _pending(std::move(f._pending)) {
     f._domain = nullptr;
     f._partition = 0.0;
 }
@@ -195,10 +202,30 @@ Factor &Factor::operator=(Factor &&f) noexcept {
         _domain = f._domain;
         _values = std::move(f._values);
         _partition = f._partition;
+        _pending = std::move(f._pending);
         f._domain = nullptr;
         f._partition = 0.0;
     }
     return *this;
+}
+void Factor::resolve_partition() const {
+    if (!_pending) return;
+    double p = 0;                                   // sequential fp64 adds from 0.0
+    if (!_pending->in) {
+        for (double x : _values) p += x;
+    } else {
+        const std::vector<double> &in = *_pending->in;
+        const uint64_t k = _pending->k, lo = _pending->lo, hi = in.size() / (k * lo);
+        for (uint64_t h = 0; h < hi; ++h)
+            for (uint64_t l = 0; l < lo; ++l)
+                for (uint64_t v = 0; v < k; ++v) p += in[(h * k + v) * lo + l];
+    }
+    _partition = p;
+    _pending.reset();
+}
+double Factor::partition() const {
+    resolve_partition();
+    return _partition;
 }
 Factor &Factor::operator=(const Factor &f) {
     if (this != &f) {
@@ -214,6 +241,7 @@ const double &Factor::operator[](uint64_t i) const {
     throw "Factor::operator[]: Index out of range.";
 }
 double &Factor::operator[](uint64_t i) {
+    resolve_partition();                            // the sum of the values as the op made them
     if (i < size()) return _values[i];
     throw "Factor::operator[]: Index out of range.";
 }
@@ -223,7 +251,7 @@ double Factor::max() const {
     return m;
 }
 double Factor::min() const {
-    double m = _partition;
+    double m = partition();
     for (double p : _values) m = p < m ? p : m;
     return m;
 }
@@ -235,11 +263,11 @@ Factor Factor::product(const Factor &f) const {
     OutBuf out(nd->size());
     std::vector<int> av = ids(*_domain), bv = ids(*f._domain), ov = ids(*nd);
     check(bnpp_product(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
-                       bv.data(), out.p, (int)ov.size(), ov.data(), out.sum()),
+                       bv.data(), out.p, (int)ov.size(), ov.data(), nullptr),
           "product");
-    double p = 0;
-    std::vector<double> vals = download(out, p);
-    return Factor(nd, std::move(vals), p);
+    Factor r(nd, download(out), 0.0);
+    r._pending = std::make_shared<PendingSum>();
+    return r;
 }
 
 Factor Factor::divide(const Factor &f) const {
@@ -249,11 +277,11 @@ Factor Factor::divide(const Factor &f) const {
     OutBuf out(nd->size());
     std::vector<int> av = ids(*_domain), bv = ids(*f._domain), ov = ids(*nd);
     check(bnpp_divide(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), b->p, (int)bv.size(),
-                      bv.data(), out.p, (int)ov.size(), ov.data(), out.sum()),
+                      bv.data(), out.p, (int)ov.size(), ov.data(), nullptr),
           "divide");
-    double p = 0;
-    std::vector<double> vals = download(out, p);
-    return Factor(nd, std::move(vals), p);
+    Factor r(nd, download(out), 0.0);
+    r._pending = std::make_shared<PendingSum>();
+    return r;
 }
 
 Factor Factor::sum_out(const Variable *variable) const {
@@ -264,11 +292,19 @@ Factor Factor::sum_out(const Variable *variable) const {
     OutBuf out(nd->size());
     std::vector<int> av = ids(*_domain), ov = ids(*nd);
     check(bnpp_sum_out(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), (int)variable->id(),
-                       out.p, (int)ov.size(), ov.data(), out.sum()),
+                       out.p, (int)ov.size(), ov.data(), nullptr),
           "sum_out");
-    double p = 0;
-    std::vector<double> vals = download(out, p);
-    return Factor(nd, std::move(vals), p);
+    Factor r(nd, download(out), 0.0);
+    auto ps = std::make_shared<PendingSum>();
+    ps->in = std::make_shared<const std::vector<double>>(_values);
+    for (unsigned i = 0; i < _domain->width(); ++i)
+        if ((*_domain)[i] == variable) {                 // removal by pointer identity (domain.cpp:57)
+            ps->k = variable->size();
+            ps->lo = 1;
+            for (unsigned j = i + 1; j < _domain->width(); ++j) ps->lo *= (*_domain)[j]->size();
+        }
+    r._pending = ps;
+    return r;
 }
 
 Factor Factor::conditioning(const std::unordered_map<unsigned, unsigned> &evidence) const {
@@ -283,15 +319,16 @@ Factor Factor::conditioning(const std::unordered_map<unsigned, unsigned> &eviden
     OutBuf out(nd->size());
     std::vector<int> av = ids(*_domain);
     check(bnpp_condition(ctx(), nullptr, BNPP_F64, (int)cards.size(), cards.data(), a->p, (int)av.size(), av.data(), (int)ev_vars.size(),
-                         ev_vars.data(), ev_vals.data(), out.p, out.sum()),
+                         ev_vars.data(), ev_vals.data(), out.p, nullptr),
           "conditioning");
-    double p = 0;
-    std::vector<double> vals = download(out, p);
-    return Factor(nd, std::move(vals), p);
+    Factor r(nd, download(out), 0.0);
+    r._pending = std::make_shared<PendingSum>();
+    return r;
 }
 
 Factor Factor::normalize() const {
     Factor f(*this);
+    f.resolve_partition();
     for (double &v : f._values) v = v / f._partition;
     f._partition = 1.0;
     return f;
@@ -299,7 +336,7 @@ Factor Factor::normalize() const {
 
 std::ostream &operator<<(std::ostream &os, const Factor &f) {      // factor.cpp:291-321
     const Domain &d = *f._domain;
-    os << "Factor(width:" << f.width() << ", size:" << f.size() << ", partition:" << f._partition << ")" << std::endl;
+    os << "Factor(width:" << f.width() << ", size:" << f.size() << ", partition:" << f.partition() << ")" << std::endl;
     for (unsigned i = 0; i < d.width(); ++i) os << d[i]->id() << " ";
     os << std::endl;
     std::vector<unsigned> val(d.width(), 0);

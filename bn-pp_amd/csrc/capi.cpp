@@ -150,12 +150,19 @@ int run_single(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &c
 // on the same stream: the terms of the inputs' chain product (or in[0] /
 // in[1]) over `dims` -- the reference's output scope order, last fastest --
 // with elim_var's values inner, added one at a time in that order.
+// checked before the op is launched, so an unsupported out_sum never leaves
+// an op that ran behind an error status
+int seq_sum_supported(const double *out_sum, size_t n_dims, size_t n_in) {
+    if (out_sum && (n_dims > (size_t)kSeqMaxDims || n_in > (size_t)kMaxIn))
+        return set_err(BNPP_ERR_UNSUPPORTED, "out_sum: at most 32 output variables");
+    return BNPP_OK;
+}
+
 int run_seq_sum(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &cards, const std::vector<View> &in,
                 const std::vector<const void *> &ptrs, const std::vector<int> &dims, int elim_var, bool divide,
                 double *out_sum) {
     if (!out_sum) return BNPP_OK;
-    if (dims.size() > (size_t)kSeqMaxDims || in.size() > (size_t)kMaxIn)
-        return set_err(BNPP_ERR_UNSUPPORTED, "out_sum: at most 32 output variables");
+    if (int rc = seq_sum_supported(out_sum, dims.size(), in.size())) return rc;
     SeqSumArgs a;
     std::memset(&a, 0, sizeof a);
     const int64_t eb = dtype == BNPP_F32 ? 4 : 8;
@@ -1051,6 +1058,7 @@ int bnpp_bucket_eliminate(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, c
     if (us != os) return set_err(BNPP_ERR_INVALID, "output scope must be the union of the inputs minus elim_var");
     b.out_vars = ov;
     b.out_table = n_in;
+    if (int rc = seq_sum_supported(out_sum, u.size(), b.in.size())) return rc;
     int rc = run_single(ctx, stream, dtype, cv, b, ptrs, out_table);
     if (rc == BNPP_OK) rc = run_seq_sum(ctx, stream, dtype, cv, b.in, ptrs, u, elim_var, false, out_sum);
     return rc;
@@ -1088,6 +1096,7 @@ int bnpp_divide(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const int *
     bs.out_vars = ov;
     bs.out_table = 2;
     bs.divide = true;
+    if (int rc = seq_sum_supported(out_sum, u.size(), bs.in.size())) return rc;
     int rc = run_single(ctx, stream, dtype, cv, bs, {a, b}, out);
     if (rc == BNPP_OK) rc = run_seq_sum(ctx, stream, dtype, cv, bs.in, {a, b}, u, -1, true, out_sum);
     return rc;
@@ -1121,6 +1130,7 @@ int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const in
     b.in.push_back(conditioned_view(0, s, cv, ev));
     b.out_vars = b.in[0].vars;
     b.out_table = 1;
+    if (int rc = seq_sum_supported(out_sum, b.out_vars.size(), b.in.size())) return rc;
     int rc = run_single(ctx, stream, dtype, cv, b, {in}, out);
     if (rc == BNPP_OK) rc = run_seq_sum(ctx, stream, dtype, cv, b.in, {in}, b.out_vars, -1, false, out_sum);
     return rc;

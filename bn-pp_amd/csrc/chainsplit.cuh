@@ -422,7 +422,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     // kChainBel: the forward message at this lane's 16 output positions of the
     // tile whose rest offset is `to` (the same scattered addresses as the
     // stores), loaded before the tile's exchange so they arrive behind it --
-    // in one-run launches before the next tile's row prefetch (lam_early,
+    // in one-run launches before the next tile's row prefetch (BM = 1,
     // below).  They are most of a fused run's extra time (10.4 ms per run
     // against 6.3 ms unfused; 10.9 ms when issued after the prefetch, 6.9 ms
     // with the loads removed); loading them a whole tile ahead needed 128
@@ -435,13 +435,14 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             for (int e = 0; e < 16; ++e) lv[e] = gload(lb + (int64_t)slab_e(e) * c.d_slab);
         }
     };
-    // one-run backward launches issue a tile's lam loads before the next
-    // tile's row loads (lam_early): waiting for lam then leaves those in
-    // flight, where loads issued after them drained them
-    bool lam_early = false;
-    auto run_tile = [&](float (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
-        if constexpr (FORM == kChainBwd && DENSE) {
-            if (c.bel && !lam_early) load_lam(tout);
+    // BM (belief mode): 0 = the run forms no belief; 1 = it does and the
+    // caller issued the tile's lam loads (one-run launches: before the next
+    // tile's row loads, so waiting for lam leaves those in flight); 2 = check
+    // c.bel at run time and load lam here (multi-run launches)
+    auto run_tile = [&](auto bmc, float (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
+        constexpr int BM = decltype(bmc)::value;
+        if constexpr (FORM == kChainBwd && DENSE && BM == 2) {
+            if (c.bel) load_lam(tout);
         }
         if constexpr (FORM == kChainBwd) {
             // rows through the image, then this lane's 16 entries (slots 4.. = w)
@@ -530,7 +531,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 T *wb = c.out + tout + (int64_t)wsl * c.d_slab + lane;
 #pragma unroll
                 for (int e = 0; e < 16; ++e) store_n<T, 1, kNtStore, true>(wb + (int64_t)slab_e(e) * c.d_slab, &t[e]);
-                if (c.bel) {
+                if (BM == 1 || (BM == 2 && c.bel)) {
                     // belief of rest entry r = lane: lam * pi per slab s into row r
                     // of the image (free: every wave read its rows before the
                     // exchange barrier), then one wave adds each row's 2^F
@@ -583,25 +584,39 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         // the wait counts stay static) before the current tile is computed (two
         // tiles ahead, as the forward form: 6.37-6.42 against 6.33-6.41 ms per
         // 2^32-entry message, profiles/r04_split_ab.txt)
+        //
+        // The loop's memory waits are what the compiler derives from its
+        // scoreboard, so the loop is shaped for it: (1) the prologue's row
+        // loads are waited for before the loop -- pending at the loop header
+        // they merged with the back edge into a wait, at the top of every
+        // tile, for the previous tile's slab stores and this tile's lam loads;
+        // (2) the lam loads are unconditional in a loop of their own -- issued
+        // under a branch, the merge at the branch's join took the path without
+        // them and drained them at the top of the tile as well
         decode(vb, in_off, out_off, gb);
         issue(in_off, rg);
-        lam_early = c.bel != nullptr;
-        while (true) {
-            float t[16];
+        __builtin_amdgcn_s_waitcnt(0x0f70);                // vmcnt(0): the first tile's rows
+        auto loop = [&](auto belc) {
+            constexpr bool BEL = decltype(belc)::value;
+            while (true) {
+                float t[16];
 #pragma unroll
-            for (int e = 0; e < 16; ++e) t[e] = rg[e];
-            if (lam_early) {
+                for (int e = 0; e < 16; ++e) t[e] = rg[e];
+                if constexpr (BEL) {
+                    decode(vb, in_off, out_off, gb);
+                    load_lam(tout);
+                }
+                const int64_t vbn = vb + gridDim.x;
+                decode(vbn < total_vblocks ? vbn : total_vblocks - 1, in_off, out_off, gb);
+                issue(in_off, rg);
                 decode(vb, in_off, out_off, gb);
-                load_lam(tout);
+                run_tile(std::integral_constant<int, BEL ? 1 : 0>{}, t, out_off, gb);
+                vb = vbn;
+                if (vb >= total_vblocks) break;
             }
-            const int64_t vbn = vb + gridDim.x;
-            decode(vbn < total_vblocks ? vbn : total_vblocks - 1, in_off, out_off, gb);
-            issue(in_off, rg);
-            decode(vb, in_off, out_off, gb);
-            run_tile(t, out_off, gb);
-            vb = vbn;
-            if (vb >= total_vblocks) break;
-        }
+        };
+        if (DENSE && c.bel) loop(std::true_type{});
+        else loop(std::false_type{});
     } else if constexpr (!MULTI) {
         // one bucket, forward form: the next tile's loads go into registers at
         // the top of a tile and, once the tile is done, into this lane's own
@@ -632,7 +647,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             decode(vbn < last ? vbn : last, in_off, out_off, gb);
             issue(in_off, p);
             decode(vb, in_off, out_off, gb);
-            run_tile(t, out_off, gb);
+            run_tile(std::integral_constant<int, 0>{}, t, out_off, gb);
             stage();
             vb = vbn;
             if (vb >= total_vblocks) break;
@@ -642,7 +657,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             float t[16];
             decode(vb, in_off, out_off, gb);
             issue(in_off, t);
-            run_tile(t, out_off, gb);
+            run_tile(std::integral_constant<int, 2>{}, t, out_off, gb);
             const int64_t vbn = vb + gridDim.x;
             if (vbn >= total_vblocks) break;
             if (vbn >= cur_end) {                          // the next tile is in another bucket of the level

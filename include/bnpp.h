@@ -110,7 +110,13 @@ int bnpp_out_scope(int n_in, const int *in_ndims, const int *const *in_vars, int
  * terms/s): ask for it only where the caller reads partition().  Single ops
  * compute the reference's unscaled values, so there is no log10 scale to
  * return (the VE entry points below carry theirs).  fp32 tables: the fp32
- * terms, widened, summed in fp64. */
+ * terms, widened, summed in fp64.  At most 32 output variables with out_sum
+ * (BNPP_ERR_UNSUPPORTED otherwise, checked before the op is launched).  One
+ * case the ABI cannot reproduce: Factor::sum_out of a variable NOT in the
+ * scope returns a copy that keeps the input's STORED _partition
+ * (factor.cpp:185-188), which may differ from the linear sum of its entries
+ * (e.g. 1.0 after normalize); out_sum is always the linear sum -- a caller
+ * that tracks _partition (the C++ mirror does) keeps its own value there. */
 /* Fused bucket:  out = sum_{elim_var} prod_i in_i   — replaces the bucket body of
  * BN::variable_elimination (model.cpp:414-418):
  *     Factor prod(1.0); for (pf : bucket) prod *= *pf; prod.sum_out(var)

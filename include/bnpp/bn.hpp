@@ -13,6 +13,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <ostream>
 #include <string>
 #include <unordered_map>
@@ -76,7 +77,7 @@ public:
     const Domain &domain() const { return *_domain; }
     uint64_t size() const { return _domain->size(); }
     unsigned width() const { return _domain->width(); }
-    double partition() const { return _partition; }
+    double partition() const;                    // factor.hh:26 (computed on first read)
     const double &operator[](uint64_t i) const;
     double &operator[](uint64_t i);
     const std::vector<double> &values() const { return _values; }
@@ -91,9 +92,17 @@ public:
     friend std::ostream &operator<<(std::ostream &os, const Factor &f);
 
 private:
+    // The reference computes _partition with every op (factor.cpp:129-139,
+    // 161-172, 196-208, 226-236); here an op leaves it pending and the first
+    // read (partition(), normalize(), min(), printing, a mutable operator[])
+    // computes it on the host in the reference's order, so an op whose
+    // partition nobody reads costs its kernel and transfers only.
+    struct PendingSum;
+    void resolve_partition() const;
     const Domain *_domain;
     std::vector<double> _values;
-    double _partition;
+    mutable double _partition;
+    mutable std::shared_ptr<const PendingSum> _pending;
 };
 
 // The GPU engine's precision for Model/BN inference (default fp64, bit-exact

@@ -17,3 +17,8 @@ print('value', d['value'], 'frac', d['roofline']['frac'], 'mar warm', d['mar']['
 print('secondary', json.dumps(d['mar']['secondary']))
 r=json.loads(open('$OUT/rehearse2.json').read().strip().splitlines()[-1])
 print('rehearse n_gpus', r['n_gpus'], r['backend'], 'sliced', json.dumps(r['mar'].get('sliced')))"
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/mar32 -o mar32 --output-format csv -- python3 $R/tools/mar_grid.py --rows 32 --cols 32 --check 0 --reps 2 > $OUT/mar32.log 2>&1 || exit 1
+cd $R
+grep -E '"mar"|wall' $OUT/mar32.log | cut -c1-200
+head -12 $(find $OUT/mar32 -name "*kernel_stats.csv") | cut -c1-200
