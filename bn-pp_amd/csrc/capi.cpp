@@ -1118,10 +1118,14 @@ int bnpp_condition(bnpp_ctx *ctx, void *stream, int dtype, int n_cards, const in
     if (!valid_scope(ndims, vars, cards, n_cards)) return set_err(BNPP_ERR_INVALID, "bad scope");
     std::vector<int> cv(cards, cards + n_cards);
     std::vector<int> ev(n_cards, -1);
+    std::vector<char> in_scope(n_cards, 0);
+    for (int i = 0; i < ndims; ++i) in_scope[vars[i]] = 1;
     for (int i = 0; i < n_ev; ++i) {
         int v = ev_vars[i];
         if (v < 0) return set_err(BNPP_ERR_INVALID, "bad evidence variable");
-        if (v >= n_cards) continue;                         // not in this factor's scope
+        // evidence on a variable outside the scope does not touch the factor
+        // (Domain(d, ev) looks up scope variables only, domain.cpp:74-90)
+        if (v >= n_cards || !in_scope[v]) continue;
         if (ev_vals[i] < 0 || ev_vals[i] >= cv[v]) return set_err(BNPP_ERR_INVALID, "evidence value out of range");
         ev[v] = ev_vals[i];
     }
