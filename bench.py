@@ -323,11 +323,17 @@ def free_port() -> int:
 def self_launch(n: int, argv) -> int:
     """`python bench.py --gpus N` outside a launcher: start N fresh rank
     processes (children, before this process touches the GPU -- no exec) and
-    pass their exit status on.  Rank 0's JSON line reaches stdout through the
-    inherited descriptor; the launcher's own chatter goes to stderr."""
+    pass their exit status on.  Rank 0's JSON line is relayed to stdout; the
+    launcher's and the ranks' other output goes to stderr."""
     env = dict(os.environ)
     env["BNPP_BENCH_CHILD"] = "1"
-    return subprocess.run(launcher_cmd(n, free_port(), argv), env=env).returncode
+    # the ranks' stdout is filtered: the JSON record goes to stdout, anything
+    # else (gloo's connection notices, for one) to stderr
+    p = subprocess.Popen(launcher_cmd(n, free_port(), argv), env=env, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return p.wait()
 
 
 def parse_args(argv=None):
