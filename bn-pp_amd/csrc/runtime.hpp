@@ -2,7 +2,10 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -68,6 +71,43 @@ hipError_t launch_bp_flood_marginals(const BpFlood &a, hipStream_t stream);
 
 enum DType { kF64 = 0, kF32 = 1 };
 
+// An arena reserved as one virtual range and backed chunk by chunk (HIP's
+// virtual-memory API) by a helper thread, in the order the schedule first
+// touches the chunks.  A cold call's hipMalloc of the whole arena waited for
+// the driver to clear HBM that any process freed shortly before (~36 GB/s of
+// backlog, profiles/r04_map_probe.log) before the first kernel could run;
+// mapped chunk by chunk, each chunk waits only for its own share of that
+// backlog, and the launch loop blocks only before a level that touches a
+// chunk not mapped yet -- the device meanwhile runs the levels already
+// enqueued.  Nothing else may allocate while the helper maps (a small
+// hipMalloc waits behind it), so every small buffer of the call is made
+// before the helper starts.
+struct VmmArena {
+    void *base = nullptr;
+    size_t bytes = 0;                  // reserved (a multiple of `chunk`)
+    size_t chunk = 0;
+    int device = 0;
+    std::vector<hipMemGenericAllocationHandle_t> handles;   // per chunk, once created
+    std::vector<char> created;
+    std::vector<int> order;            // chunks in mapping order
+    std::atomic<int> mapped{0};        // prefix of `order` mapped and accessible
+    std::atomic<int> failed{0};
+    hipError_t err = hipSuccess;
+    double map_ms = 0;                 // the helper's time (overlapped with the run)
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+};
+// reserve `bytes` of address space; false when the device has no VMM support
+bool vmm_reserve(int device, size_t bytes, VmmArena &a);
+// start the helper: map the chunks in `order` (chunks missing from it last)
+void vmm_start(VmmArena &a, std::vector<int> order);
+// block until the first `prefix` chunks of the order are mapped: 0, or the
+// helper's error; adds the time blocked to *wait_ms
+hipError_t vmm_wait(VmmArena &a, int prefix, double *wait_ms);
+// join the helper, unmap and release every chunk, free the range
+void vmm_release(VmmArena &a);
+
 struct Context {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -78,6 +118,7 @@ struct Context {
     // allocator the context holds on to it until it is destroyed
     void *arena_cache = nullptr;
     int64_t arena_cache_bytes = 0;
+    std::shared_ptr<VmmArena> arena_cache_vmm;          // when the cached arena is VMM-backed
     // small device buffers (sources, descriptors, dims pool, metadata, results)
     // kept for reuse: a one-shot call otherwise pays ~10 hipMalloc / hipFree
     // pairs (hipFree synchronises), several ms of a small model's PR
@@ -145,6 +186,11 @@ struct Program {
     bool arena_cached = false;          // arena is the context's cache (not freed with the program)
     bool arena_reused = false;          // ... and was already allocated before this program
     double arena_alloc_ms = 0;          // hipMalloc of the arena (0 when reused), incl. the driver's HBM clearing wait
+                                        // (VMM arenas: the address reservation only)
+    std::shared_ptr<VmmArena> vmm;      // VMM-backed arena (owned here, or shared with the context's cache)
+    std::vector<std::vector<int>> vmm_need;   // per part, per group: chunks of vmm->order it touches by then
+    bool vmm_pending = false;           // this program started the helper: its launch waits per group
+    double vmm_wait_ms = 0;             // launch loop time blocked on the helper (last launch)
     void *results = nullptr;
     size_t results_cap = 0;
     int64_t results_bytes = 0;
@@ -156,7 +202,10 @@ struct Program {
 int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out);
 void free_sources(Context &ctx, DeviceSources &s);
 int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex, void *shared_arena = nullptr);
-int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks = nullptr);
+// vmm / need: a VMM arena still being mapped and, per group, the prefix of
+// its mapping order the group needs (Program::vmm_need)
+int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks = nullptr, VmmArena *vmm = nullptr,
+           const std::vector<int> *need = nullptr, double *wait_ms = nullptr);
 // waits for `stream`, downloads result tables: values as stored (double) and the exp2 scale
 int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<std::vector<double>> &vals,
                   std::vector<int64_t> &exp2);

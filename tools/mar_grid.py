@@ -49,6 +49,7 @@ def main():
         worst = max(abs(sum(p) - 1.0) for p in marg.values())
         print(json.dumps({"phase": "mar", "rep": rep, "instance": "ising%dx%d-col" % (r, c), "dtype": args.dtype,
                           "uptime_ms": up, "wall_ms": wall, "max_sum_err": worst,
+                          "phases": bnpp.last_timing(),
                           "p0": marg[0], "p_mid": marg[(r // 2) * c + c // 2]}), flush=True)
     if args.check > 0:
         lz = bnpp.partition(ctx, m, {}, "mf", dt, order=col)[0]
