@@ -876,11 +876,11 @@ void oneshot_done(bnpp_ctx *ctx, bool cache_ok, uint64_t key, bnpp_job *job, int
 }
 
 // launch / run+fetch / free / total of a call whose create_job filled phases 0-2
-// the arena's mapping (VMM arenas, runtime.cpp VmmArena) during the job's
-// last launch: the launch loop's time blocked on it, and the helper's own time
+// the arena's mapping during the job's last launch (VMM arenas,
+// runtime.cpp VmmArena): all of it, and the part before the first level
 void record_map_timing(const bnpp_job *job) {
-    g_timing[9] = job ? job->pg.vmm_wait_ms : 0.0;
-    g_timing[10] = job && job->pg.vmm && !job->pg.arena_reused ? job->pg.vmm->map_ms : 0.0;
+    g_timing[9] = job ? job->pg.vmm_map_ms : 0.0;
+    g_timing[10] = job ? job->pg.vmm_first_ms : 0.0;
 }
 
 void record_call_timing(double t0, double t1, double t2, double t3) {

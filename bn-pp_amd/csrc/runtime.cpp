@@ -62,61 +62,39 @@ bool vmm_reserve(int device, size_t bytes, VmmArena &a) {
     return true;
 }
 
-void vmm_start(VmmArena &a, std::vector<int> order) {
+void vmm_set_order(VmmArena &a, std::vector<int> order) {
     const int n = (int)a.handles.size();
     std::vector<char> seen(n, 0);
     for (int c : order) seen[c] = 1;
     for (int c = 0; c < n; ++c)
         if (!seen[c]) order.push_back(c);
     a.order = std::move(order);
-    a.mapped.store(0);
-    a.failed.store(0);
-    VmmArena *pa = &a;
-    a.th = std::thread([pa]() {
-        VmmArena &a = *pa;
-        const auto t0 = std::chrono::steady_clock::now();
-        hipError_t e = hipSetDevice(a.device);
-        const hipMemAllocationProp prop = vmm_prop(a.device);
-        hipMemAccessDesc acc = {};
-        acc.location = prop.location;
-        acc.flags = hipMemAccessFlagsProtReadWrite;
-        for (size_t i = 0; i < a.order.size() && e == hipSuccess; ++i) {
-            const int c = a.order[i];
-            void *p = static_cast<unsigned char *>(a.base) + (size_t)c * a.chunk;
-            // the driver hands out HBM cleared: this is where a chunk waits
-            // for the clearing of memory freed shortly before
-            if ((e = hipMemCreate(&a.handles[c], a.chunk, &prop, 0)) != hipSuccess) break;
-            a.created[c] = 1;
-            if ((e = hipMemMap(p, a.chunk, 0, a.handles[c], 0)) != hipSuccess) break;
-            a.created[c] = 2;
-            if ((e = hipMemSetAccess(p, a.chunk, &acc, 1)) != hipSuccess) break;
-            {
-                std::lock_guard<std::mutex> g(a.mu);
-                a.mapped.store((int)i + 1);
-            }
-            a.cv.notify_all();
-        }
-        std::lock_guard<std::mutex> g(a.mu);
-        a.map_ms = ms_since(t0);
-        if (e != hipSuccess) {
-            a.err = e;
-            a.failed.store(1);
-        }
-        a.cv.notify_all();
-    });
 }
 
-hipError_t vmm_wait(VmmArena &a, int prefix, double *wait_ms) {
-    if (a.mapped.load() >= prefix) return hipSuccess;
+hipError_t vmm_map_to(VmmArena &a, int prefix, double *ms) {
+    if (a.mapped >= prefix) return hipSuccess;
     const auto t0 = std::chrono::steady_clock::now();
-    std::unique_lock<std::mutex> lk(a.mu);
-    a.cv.wait(lk, [&] { return a.mapped.load() >= prefix || a.failed.load(); });
-    if (wait_ms) *wait_ms += ms_since(t0);
-    return a.mapped.load() >= prefix ? hipSuccess : (a.err != hipSuccess ? a.err : hipErrorOutOfMemory);
+    const hipMemAllocationProp prop = vmm_prop(a.device);
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    hipError_t e = hipSuccess;
+    for (; a.mapped < prefix && a.mapped < (int)a.order.size(); ++a.mapped) {
+        const int c = a.order[a.mapped];
+        void *p = static_cast<unsigned char *>(a.base) + (size_t)c * a.chunk;
+        // the driver hands out HBM cleared: this is where a chunk waits for
+        // the clearing of memory freed shortly before
+        if ((e = hipMemCreate(&a.handles[c], a.chunk, &prop, 0)) != hipSuccess) break;
+        a.created[c] = 1;
+        if ((e = hipMemMap(p, a.chunk, 0, a.handles[c], 0)) != hipSuccess) break;
+        a.created[c] = 2;
+        if ((e = hipMemSetAccess(p, a.chunk, &acc, 1)) != hipSuccess) break;
+    }
+    if (ms) *ms += ms_since(t0);
+    return e;
 }
 
 void vmm_release(VmmArena &a) {
-    if (a.th.joinable()) a.th.join();
     (void)hipSetDevice(a.device);
     for (size_t c = 0; c < a.handles.size(); ++c) {
         void *p = static_cast<unsigned char *>(a.base) + c * a.chunk;
@@ -357,7 +335,7 @@ static int run_xchg(Context &ctx, Executable &ex, const Schedule::Group &g, hipS
 }
 
 int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks, VmmArena *vmm,
-           const std::vector<int> *need, double *wait_ms) {
+           const std::vector<int> *need, double *map_ms, double *first_ms) {
     const Schedule &sc = ex.sched;
     hipError_t err = hipMemcpyAsync(ex.d_meta, ex.d_meta0, sizeof(TableMeta) * (size_t)sc.n_tables,
                                     hipMemcpyDeviceToDevice, stream);
@@ -370,9 +348,10 @@ int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *ho
     for (size_t gi = 0; gi < sc.groups.size(); ++gi) {
         const Schedule::Group &g = sc.groups[gi];
         hipStream_t st = ls[lanes ? g.lane & 1 : 0];
-        // a VMM arena still being mapped: the group's chunks must be mapped
-        // before it is enqueued (the device keeps running the levels before it)
-        if (vmm && need && gi < need->size() && (err = vmm_wait(*vmm, (*need)[gi], wait_ms)) != hipSuccess)
+        // a VMM arena not fully mapped: the group's chunks are mapped before
+        // it is enqueued (the device keeps running the levels before it)
+        if (vmm && need && gi < need->size() &&
+            (err = vmm_map_to(*vmm, (*need)[gi], gi == 0 ? first_ms : map_ms)) != hipSuccess)
             return fail(ctx, err, "arena mapping (hipMemCreate / hipMemMap)");
         if (lanes)
             for (int e : ex.g_wait[gi])
@@ -513,13 +492,9 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
     hipError_t err = hipSetDevice(ctx.device);
     if (err != hipSuccess) return fail(ctx, err, "hipSetDevice");
     const int64_t need = std::max<int64_t>(pg.arena_bytes, 256);
-    if (use_cache && ctx.arena_cache && ctx.arena_cache_bytes >= need && ctx.arena_cache_vmm) {
-        // a VMM arena an earlier call began mapping: complete, or replaced
-        if (vmm_wait(*ctx.arena_cache_vmm, (int)ctx.arena_cache_vmm->handles.size(), nullptr) != hipSuccess)
-            drop_arena_cache(ctx);
-        else if (ctx.arena_cache_vmm->th.joinable())
-            ctx.arena_cache_vmm->th.join();
-    }
+    if (use_cache && ctx.arena_cache && ctx.arena_cache_bytes >= need && ctx.arena_cache_vmm &&
+        ctx.arena_cache_vmm->mapped < (int)ctx.arena_cache_vmm->handles.size())
+        drop_arena_cache(ctx);                           // an earlier call failed to map it all
     if (use_cache && ctx.arena_cache && ctx.arena_cache_bytes >= need) {
         pg.arena = ctx.arena_cache;
         pg.vmm = ctx.arena_cache_vmm;
@@ -605,11 +580,11 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
                 return fail(ctx, err, "hipMemcpy(copies)");
         }
     }
-    // every small buffer of the call exists now: the helper may map
+    // a new VMM arena: chunks mapped by the launch as levels first need them
     if (pg.vmm && !pg.arena_reused) {
         std::vector<int> order;
         vmm_plan(pg, eb, order, pg.vmm_need);
-        vmm_start(*pg.vmm, std::move(order));
+        vmm_set_order(*pg.vmm, std::move(order));
         pg.vmm_pending = true;
     }
     return 0;
@@ -618,11 +593,12 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
 int launch_program(Context &ctx, Program &pg, hipStream_t stream) {
     const int64_t eb = pg.dtype == kF32 ? 4 : 8;
     (void)eb;
-    pg.vmm_wait_ms = 0;
+    pg.vmm_map_ms = pg.vmm_first_ms = 0;
     VmmArena *vmm = pg.vmm_pending ? pg.vmm.get() : nullptr;
     for (size_t b = 0; b < pg.parts.size(); ++b) {
         Executable &ex = pg.parts[b];
-        int rc = launch(ctx, ex, stream, &pg.hooks, vmm, vmm ? &pg.vmm_need[b] : nullptr, &pg.vmm_wait_ms);
+        int rc = launch(ctx, ex, stream, &pg.hooks, vmm, vmm ? &pg.vmm_need[b] : nullptr, &pg.vmm_map_ms,
+                        b == 0 ? &pg.vmm_first_ms : &pg.vmm_map_ms);
         if (rc) return rc;
         if (ex.n_copies > 0) {
             hipError_t err = launch_copies(ex.d_copies, ex.n_copies, ex.copy_max_bytes, stream);
@@ -630,11 +606,11 @@ int launch_program(Context &ctx, Program &pg, hipStream_t stream) {
         }
     }
     if (vmm) {
-        // the rest of the range (if any chunk went untouched) before anything
-        // else may allocate or copy; later launches of this program need no wait
-        hipError_t err = vmm_wait(*vmm, (int)vmm->handles.size(), &pg.vmm_wait_ms);
+        // the rest of the range (chunks no level touched): later launches of
+        // this program, and later programs in the cached arena, map nothing
+        hipError_t err = vmm_map_to(*vmm, (int)vmm->handles.size(), &pg.vmm_map_ms);
         if (err != hipSuccess) return fail(ctx, err, "arena mapping (hipMemCreate / hipMemMap)");
-        if (vmm->th.joinable()) vmm->th.join();
+        pg.vmm_map_ms += pg.vmm_first_ms;
         pg.vmm_pending = false;
     }
     return 0;

@@ -2,8 +2,6 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
-#include <atomic>
-#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -72,40 +70,32 @@ hipError_t launch_bp_flood_marginals(const BpFlood &a, hipStream_t stream);
 enum DType { kF64 = 0, kF32 = 1 };
 
 // An arena reserved as one virtual range and backed chunk by chunk (HIP's
-// virtual-memory API) by a helper thread, in the order the schedule first
-// touches the chunks.  A cold call's hipMalloc of the whole arena waited for
-// the driver to clear HBM that any process freed shortly before (~36 GB/s of
+// virtual-memory API) as the launch loop reaches the first level that touches
+// each chunk.  A cold call's hipMalloc of the whole arena waited for the
+// driver to clear HBM that any process freed shortly before (~36 GB/s of
 // backlog, profiles/r04_map_probe.log) before the first kernel could run;
-// mapped chunk by chunk, each chunk waits only for its own share of that
-// backlog, and the launch loop blocks only before a level that touches a
-// chunk not mapped yet -- the device meanwhile runs the levels already
-// enqueued.  Nothing else may allocate while the helper maps (a small
-// hipMalloc waits behind it), so every small buffer of the call is made
-// before the helper starts.
+// mapped on demand, a chunk waits only for its own share of that backlog,
+// while the device runs the levels already enqueued before it.  The mapping
+// is done by the launching thread itself: a helper thread mapping
+// concurrently blocked the launch loop anyway (kernel code objects load on
+// first launch and wait behind the helper's allocation: profiles/r05_vmm_helper.log).
 struct VmmArena {
     void *base = nullptr;
     size_t bytes = 0;                  // reserved (a multiple of `chunk`)
     size_t chunk = 0;
     int device = 0;
     std::vector<hipMemGenericAllocationHandle_t> handles;   // per chunk, once created
-    std::vector<char> created;
+    std::vector<char> created;         // 0 none, 1 created, 2 mapped
     std::vector<int> order;            // chunks in mapping order
-    std::atomic<int> mapped{0};        // prefix of `order` mapped and accessible
-    std::atomic<int> failed{0};
-    hipError_t err = hipSuccess;
-    double map_ms = 0;                 // the helper's time (overlapped with the run)
-    std::thread th;
-    std::mutex mu;
-    std::condition_variable cv;
+    int mapped = 0;                    // prefix of `order` mapped and accessible
 };
 // reserve `bytes` of address space; false when the device has no VMM support
 bool vmm_reserve(int device, size_t bytes, VmmArena &a);
-// start the helper: map the chunks in `order` (chunks missing from it last)
-void vmm_start(VmmArena &a, std::vector<int> order);
-// block until the first `prefix` chunks of the order are mapped: 0, or the
-// helper's error; adds the time blocked to *wait_ms
-hipError_t vmm_wait(VmmArena &a, int prefix, double *wait_ms);
-// join the helper, unmap and release every chunk, free the range
+// the mapping order (chunks missing from `order` go last)
+void vmm_set_order(VmmArena &a, std::vector<int> order);
+// map the chunks of the order up to `prefix`; adds the time spent to *ms
+hipError_t vmm_map_to(VmmArena &a, int prefix, double *ms);
+// unmap and release every chunk, free the range
 void vmm_release(VmmArena &a);
 
 struct Context {
@@ -189,8 +179,9 @@ struct Program {
                                         // (VMM arenas: the address reservation only)
     std::shared_ptr<VmmArena> vmm;      // VMM-backed arena (owned here, or shared with the context's cache)
     std::vector<std::vector<int>> vmm_need;   // per part, per group: chunks of vmm->order it touches by then
-    bool vmm_pending = false;           // this program started the helper: its launch waits per group
-    double vmm_wait_ms = 0;             // launch loop time blocked on the helper (last launch)
+    bool vmm_pending = false;           // chunks still unmapped: the launch maps them as levels need them
+    double vmm_map_ms = 0;              // last launch: time mapping chunks between levels (device busy meanwhile)
+    double vmm_first_ms = 0;            // ... of which before the first level (exposed)
     void *results = nullptr;
     size_t results_cap = 0;
     int64_t results_bytes = 0;
@@ -202,10 +193,12 @@ struct Program {
 int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out);
 void free_sources(Context &ctx, DeviceSources &s);
 int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex, void *shared_arena = nullptr);
-// vmm / need: a VMM arena still being mapped and, per group, the prefix of
-// its mapping order the group needs (Program::vmm_need)
+// vmm / need: a VMM arena not fully mapped yet and, per group, the prefix of
+// its mapping order the group needs (Program::vmm_need), mapped before the
+// group is enqueued; map_ms / first_ms: time spent mapping (all / before
+// the part's first group)
 int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks = nullptr, VmmArena *vmm = nullptr,
-           const std::vector<int> *need = nullptr, double *wait_ms = nullptr);
+           const std::vector<int> *need = nullptr, double *map_ms = nullptr, double *first_ms = nullptr);
 // waits for `stream`, downloads result tables: values as stored (double) and the exp2 scale
 int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<std::vector<double>> &vals,
                   std::vector<int64_t> &exp2);
