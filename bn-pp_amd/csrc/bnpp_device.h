@@ -28,9 +28,12 @@ constexpr int kSplitRowsHost = 64; // rest entries per workgroup of the split ch
 // reduction scratch, the exchange table, the row image, then the packed G
 constexpr int kSplitPack = 8;
 constexpr int kSplitLdsBytes = 160 * 1024;
-constexpr int split_xch_bytes(int f) { return kSplitRowsHost * (1 << f) * 4; }
-constexpr int split_img_bytes(int f) { return kSplitRowsHost * ((1 << f) * 4 + 16); }
-constexpr int split_g_budget_bytes(int f) { return kSplitLdsBytes - 64 - split_xch_bytes(f) - split_img_bytes(f); }
+constexpr int split_xch_bytes(int f, int eb = 4) { return kSplitRowsHost * (1 << f) * eb; }
+constexpr int split_img_bytes(int f, int eb = 4) { return kSplitRowsHost * ((1 << f) * eb + 16); }
+constexpr int split_g_budget_bytes(int f, int eb = 4) {
+    return kSplitLdsBytes - 64 - split_xch_bytes(f, eb) - split_img_bytes(f, eb);
+}
+constexpr int split_max_f(int eb) { return eb == 4 ? 8 : 7; }    // longest split run per element size
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 
 // One per table (source factor or message), resident in device memory.
@@ -164,6 +167,9 @@ enum ChainDep : int32_t { kDepNext = 0, kDepPrev = 1, kDepAny = 2 };
 __host__ __device__ inline int chain_key(int form, int k, int f, int dep) {
     return 8192 + dep * 2048 + form * 256 + k * 16 + f;
 }
+// a dense backward split run forming a fused belief (kChainBel) launches its
+// own kernel: key chain_key(...) + kChainBelKey (k * 16 + f < 128 leaves the bit free)
+constexpr int kChainBelKey = 128;
 // rest entries per thread of the backward form (the forward form has 1)
 __host__ __device__ constexpr int chain_bwd_v(int n, int elem_bytes) {
     return 64 / n < 1 ? 1 : (64 / n > 16 / elem_bytes ? 16 / elem_bytes : 64 / n);

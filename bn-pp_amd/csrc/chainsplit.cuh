@@ -1,6 +1,8 @@
-// Split chain runs (gfx950): F = 5..8 consecutive sweep buckets of a binary
-// (K = 2) fp32 message fused in one pass, the 2^F-entry table of one rest
-// entry spread over W = 2^(F-4) waves of one workgroup (16 entries per lane).
+// Split chain runs (gfx950): F consecutive sweep buckets of a binary (K = 2)
+// message fused in one pass, the 2^F-entry table of one rest entry spread
+// over W = 2^(F-4) waves of one workgroup (16 entries per lane): F = 5..8 in
+// fp32, 5..7 in fp64 (an fp64 run of 8 would need a 128-KiB exchange table
+// beside its 129-KiB row image; 160 KiB of LDS hold both only up to F = 7).
 //
 // Same arithmetic as chain.cuh (one thread per rest entry, all 2^F entries in
 // its registers), which caps a run at 6 buckets (64 registers of table, 3 waves
@@ -54,6 +56,18 @@ constexpr int kMaxDevices = 64;
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 static_assert(kRedBytes == 64, "split_g_budget_bytes assumes 64 B of reduction scratch");
+template <typename T, int W>
+__device__ __forceinline__ vec_t<T, W> pack_vec(const T *x) {
+    vec_t<T, W> v;
+#pragma unroll
+    for (int k = 0; k < W; ++k) v[k] = x[k];
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T pow2_t(int e) {
+    if constexpr (sizeof(T) == 4) return __builtin_amdgcn_ldexpf(1.0f, e);
+    else return __builtin_amdgcn_ldexp(1.0, e);
+}
 
 __host__ __device__ constexpr int split_waves(int f) { return 1 << (f - 4); }
 // LDS: the exchange table and the row image side by side (so a tile needs two
@@ -63,8 +77,8 @@ __host__ __device__ constexpr int split_waves(int f) { return 1 << (f - 4); }
 // One bucket J (slot J, 0-3 in phase 1, 4..F-1 in phase 2) on the lane's 16
 // entries.  The local index e holds the local slots' digits; digit(e, p) gives
 // any slot's digit for entry e (local ones from e, the others wave-uniform).
-template <int F, int PH, int J, int DEP, typename Digit>
-__device__ __forceinline__ void split_step(float (&t)[16], const float *gp, Digit &&digit) {
+template <typename T, int F, int PH, int J, int DEP, typename Digit>
+__device__ __forceinline__ void split_step(T (&t)[16], const T *gp, Digit &&digit) {
     // place of slot J in the local index
     constexpr int PJ = PH == 1 ? (8 >> J) : (1 << (F - 1 - J));
     constexpr int Q = DEP == kDepNext ? J + 1 : J - 1;
@@ -72,10 +86,10 @@ __device__ __forceinline__ void split_step(float (&t)[16], const float *gp, Digi
     // the bucket's G values, fetched once from the packed table: [q][n][x]
     // (q: digit of slot Q), one 16-B read per q
     constexpr int NQ = HASQ ? 2 : 1;
-    float g[NQ][2][2];
+    T g[NQ][2][2];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const v4f v = *reinterpret_cast<const v4f *>(gp + 4 * q);
+        const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4> *>(gp + 4 * q);
         g[q][0][0] = v[0];
         g[q][0][1] = v[1];
         g[q][1][0] = v[2];
@@ -85,19 +99,26 @@ __device__ __forceinline__ void split_step(float (&t)[16], const float *gp, Digi
     for (int e = 0; e < 16; ++e) {
         if (e & PJ) continue;
         const int q = HASQ ? digit(e, HASQ ? Q : 0) : 0;    // constant for local slots
-        const float g00 = NQ == 2 && q ? g[NQ - 1][0][0] : g[0][0][0];
-        const float g10 = NQ == 2 && q ? g[NQ - 1][0][1] : g[0][0][1];
-        const float g01 = NQ == 2 && q ? g[NQ - 1][1][0] : g[0][1][0];
-        const float g11 = NQ == 2 && q ? g[NQ - 1][1][1] : g[0][1][1];
-        // acc = 0; acc += G(0, n) m0; acc += G(1, n) m1 for n = 0, 1 (packed
-        // pairs).  0 + p == p exactly for the non-negative p of a potential
-        // table (no -0 can arise), so the leading add is dropped.
-        const v2f m0 = {t[e], t[e]}, m1 = {t[e | PJ], t[e | PJ]};
-        const v2f gx0 = {g00, g01}, gx1 = {g10, g11};
-        const v2f p0 = gx0 * m0, p1 = gx1 * m1;
-        const v2f a = p0 + p1;
-        t[e] = a[0];
-        t[e | PJ] = a[1];
+        const T g00 = NQ == 2 && q ? g[NQ - 1][0][0] : g[0][0][0];
+        const T g10 = NQ == 2 && q ? g[NQ - 1][0][1] : g[0][0][1];
+        const T g01 = NQ == 2 && q ? g[NQ - 1][1][0] : g[0][1][0];
+        const T g11 = NQ == 2 && q ? g[NQ - 1][1][1] : g[0][1][1];
+        // acc = 0; acc += G(0, n) m0; acc += G(1, n) m1 for n = 0, 1 (fp32:
+        // packed pairs).  0 + p == p exactly for the non-negative p of a
+        // potential table (no -0 can arise), so the leading add is dropped.
+        if constexpr (sizeof(T) == 4) {
+            const v2f m0 = {t[e], t[e]}, m1 = {t[e | PJ], t[e | PJ]};
+            const v2f gx0 = {g00, g01}, gx1 = {g10, g11};
+            const v2f p0 = gx0 * m0, p1 = gx1 * m1;
+            const v2f a = p0 + p1;
+            t[e] = a[0];
+            t[e | PJ] = a[1];
+        } else {
+            const T m0 = t[e], m1 = t[e | PJ];
+            const T p00 = g00 * m0, p01 = g01 * m0, p10 = g10 * m1, p11 = g11 * m1;
+            t[e] = p00 + p10;
+            t[e | PJ] = p01 + p11;
+        }
     }
 }
 
@@ -105,10 +126,10 @@ __device__ __forceinline__ void split_step(float (&t)[16], const float *gp, Digi
 // the slab offsets of the wave's 16 phase-1 entries (forward), the output
 // strides of its 16 phase-2 entries (backward), and per bucket the strides of
 // G_j along x_j, along the dependency slot and along n_j.
-template <int F, int DEP>
+template <typename T, int F, int DEP>
 struct SplitState {
-    const float *big;
-    float *out;
+    const T *big;
+    T *out;
     const int64_t *dims;
     int64_t n_tiles, in_base, t0h, t0m;
     // the power-of-two rescale is folded into the G tables as they are staged
@@ -127,12 +148,12 @@ struct SplitState {
     int64_t d_in1, d_out1, d_slab;
     int32_t d_g1[F];
     // kChainBel (dense backward runs): the forward message and the belief table
-    const float *lam;
-    float *bel;
+    const T *lam;
+    T *bel;
 };
 
-template <int F, int DEP, bool DENSE, int FORM>
-__device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const BucketDesc &d, const int64_t *pool,
+template <typename T, int F, int DEP, bool DENSE, int FORM>
+__device__ __forceinline__ void split_load_state(SplitState<T, F, DEP> &c, const BucketDesc &d, const int64_t *pool,
                                                  TableMeta *meta, int w) {
     constexpr int HB = 8 - F;
     c.dims = pool;
@@ -178,15 +199,15 @@ __device__ __forceinline__ void split_load_state(SplitState<F, DEP> &c, const Bu
         c.glds[j] = on ? d.in_lds_off[gi] : 0;
         gi += on ? 1 : 0;
     }
-    c.big = static_cast<const float *>(meta[d.in_table[0]].ptr);
-    c.out = static_cast<float *>(meta[d.out_table].ptr);
+    c.big = static_cast<const T *>(meta[d.in_table[0]].ptr);
+    c.out = static_cast<T *>(meta[d.out_table].ptr);
     c.left = 0;
     c.lam = nullptr;
     c.bel = nullptr;
     if constexpr (DENSE && FORM == kChainBwd) {
         if (d.flags & kChainBel) {
-            c.lam = static_cast<const float *>(meta[d.in_table[d.n_in]].ptr) + d.in_base[d.n_in];
-            c.bel = static_cast<float *>(meta[d.aux_out].ptr);
+            c.lam = static_cast<const T *>(meta[d.in_table[d.n_in]].ptr) + d.in_base[d.n_in];
+            c.bel = static_cast<T *>(meta[d.aux_out].ptr);
         }
     }
 }
@@ -199,40 +220,55 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Persistent workgroups walk the level's tiles (64 rest entries each) grid-
 // stride; the next tile's message loads are issued before the current tile is
 // computed, so HBM stays busy through the exchange barriers and the stores.
-// MULTI: the launch holds several runs (descriptors); otherwise exactly one,
+// MODE 2: the launch holds several runs (descriptors); otherwise exactly one,
 // and the kernel is the one-run loop only -- without the multi-run path's
 // per-bucket restaging live in the same body, the uniform state fits the
-// scalar registers (with it: ~80 SGPRs spilled to VGPR lanes, re-read per tile)
-template <int F, int FORM, int DEP, bool DENSE, bool MULTI>
+// scalar registers (with it: ~80 SGPRs spilled to VGPR lanes, re-read per
+// tile).  One-run backward launches come in two kernels, MODE 1 forming a
+// fused belief (kChainBel) and MODE 0 not, so the plain runs' register
+// allocation does not carry the belief's (fp64: 242 against ~130 VGPRs).
+// BNPP_F64_SPLIT_WAVES (variant builds): hold the fp64 dense one-run kernels
+// without a belief to that many waves per SIMD (4: 128 VGPRs, the persistent
+// grid's 16 waves per CU, at the price of a few spilled registers; left
+// alone they take 128-164 VGPRs, 3 waves)
+#ifndef BNPP_F64_SPLIT_WAVES
+#define BNPP_F64_SPLIT_WAVES 1
+#endif
+template <typename T, int F, int FORM, int DEP, bool DENSE, int MODE>
 __global__ __launch_bounds__(64 * (1 << (F - 4)))
+__attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 && DENSE && MODE == 0 ? BNPP_F64_SPLIT_WAVES : 1)))
 void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const int64_t *__restrict__ pool,
                         TableMeta *__restrict__ meta, int64_t total_vblocks) {
-    using T = float;
+    constexpr int EB = sizeof(T);
+    constexpr int VE = 16 / EB;                            // entries per 16-B chunk
+    constexpr int IT = EB;                                 // 16-B chunks per lane per tile (16 entries)
     constexpr int W = split_waves(F);
     constexpr int N = 1 << F;
-    constexpr int ROWB = N * 4 + 16;                       // image row stride (bytes)
+    constexpr int ROWB = N * EB + 16;                      // image row stride (bytes)
     constexpr int HB = 8 - F;                              // phase 2: bits of h (n-digits 0-3 local)
     constexpr int SB = F - 4;                              // phase 2: bits of the slot combo (slots 4..F-1)
-    constexpr int CPR = N / 4;                             // 16-B chunks per row
+    constexpr int CPR = N * EB / 16;                       // 16-B chunks per row
+    static_assert(W * EB <= kRedBytes, "reduction scratch");
+    static_assert(EB == 4 || F <= 7, "fp64 split runs: F <= 7 (LDS)");
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
     T *xch = reinterpret_cast<T *>(dyn + kRedBytes);
-    unsigned char *img = dyn + kRedBytes + split_xch_bytes(F);
-    T *small = reinterpret_cast<T *>(dyn + kRedBytes + split_xch_bytes(F) + split_img_bytes(F));
+    unsigned char *img = dyn + kRedBytes + split_xch_bytes(F, EB);
+    T *small = reinterpret_cast<T *>(dyn + kRedBytes + split_xch_bytes(F, EB) + split_img_bytes(F, EB));
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // digit of slot p (4 <= p < F) in phase 1: bit (F-1-p) of w
     auto wdig = [&](int p) { return (w >> (F - 1 - p)) & 1; };
-    // the tile's 64 rows are 16 * N contiguous bytes; row traffic (backward
-    // loads, forward stores) goes in 4 instructions per lane, instruction `it`
-    // of the whole workgroup covering W contiguous KiB: 16-B chunk
-    // it * 64 W + 64 w + lane (row 16 it + w at F = 8), not 4 consecutive rows
-    // per wave (forward 6.06 -> 5.97 ms, backward 5.81 -> 5.69-5.73 ms in
-    // tools/bwdprobe.hip, profiles/r04_bwdprobe.jsonl)
+    // the tile's 64 rows are 64 * N * EB contiguous bytes; row traffic
+    // (backward loads, forward stores) goes in IT = EB instructions per lane,
+    // instruction `it` of the whole workgroup covering W contiguous KiB: 16-B
+    // chunk it * 64 W + 64 w + lane (row 16 it + w at F = 8 fp32), not IT
+    // consecutive rows per wave (forward 6.06 -> 5.97 ms, backward 5.81 ->
+    // 5.69-5.73 ms in tools/bwdprobe.hip, profiles/r04_bwdprobe.jsonl)
     auto chunk = [&](int it) { return it * 64 * W + 64 * w + lane; };
 
     int cur = -1;
     int64_t cur_begin = 0, cur_end = 0;
-    SplitState<F, DEP> c;
+    SplitState<T, F, DEP> c;
     T lmax = T(0);
     T bmax = T(0);                                         // kChainBel: the belief's running max (wave 0)
 
@@ -243,7 +279,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         cur = bi;
         cur_begin = d.vblk_begin;
         cur_end = bi + 1 < n_desc ? descs[bi + 1].vblk_begin : total_vblocks;
-        split_load_state<F, DEP, DENSE, FORM>(c, d, pool + d.dim_off, meta, w);
+        split_load_state<T, F, DEP, DENSE, FORM>(c, d, pool + d.dim_off, meta, w);
         int fs[kMaxDescIn];
         c.left = chain_fold<T>(d, meta, fs);
         // exp2 of the output: the inputs' exp2 and max exponents, plus the
@@ -262,7 +298,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             const T *src = static_cast<const T *>(meta[d.in_table[j + 1]].ptr) + d.in_base[j + 1];
             const int span = d.in_span[j + 1];
             T *dst = small + d.in_lds_off[j + 1];
-            const T sc = __builtin_amdgcn_ldexpf(1.0f, fs[j + 1]);
+            const T sc = pow2_t<T>(fs[j + 1]);
             for (int e = threadIdx.x; e < span * kSplitPack; e += 64 * W) {
                 const int si = (e >> 3) + ((e >> 2) & 1) * c.gsq[j] + ((e >> 1) & 1) * c.gsn[j] + (e & 1) * c.gsj[j];
                 const T g = si < span ? gload(src + si) : T(0);
@@ -331,7 +367,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         for (int j = 0; j < F; ++j) gb[j] = ug[j] + lane * sg[j];
     };
     // the tile's message loads (16 values per lane)
-    auto issue = [&](int64_t in_off, float (&rg)[16]) {
+    auto issue = [&](int64_t in_off, T (&rg)[16]) {
         if constexpr (DENSE && FORM == kChainFwd) {
             // slab x = (slots 0-3 = e) << (F - 4) | (slots 4.. = w), at x * S
             const T *wb = c.big + tin + (int64_t)w * c.d_slab + lane;
@@ -342,17 +378,17 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             // 64 input rows of N contiguous values at tin + row * N
             const T *big = c.big + tin;
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
+            for (int it = 0; it < IT; ++it) {
                 const int q = chunk(it);
                 const int rw = q / CPR, ch = q % CPR;
-                const vec_t<T, 4> v = vload<4, kNtLoad, true>(big + (int64_t)rw * N + 4 * ch);
+                const vec_t<T, VE> v = vload<VE, kNtLoad, true>(big + (int64_t)rw * N + VE * ch);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) rg[4 * it + k] = v[k];
+                for (int k = 0; k < VE; ++k) rg[VE * it + k] = v[k];
             }
         } else if constexpr (FORM == kChainFwd) {
             // slab of assignment (slots 0-3 = e, slots 4.. = w): uniform base + 32-bit lane offset
             const int64_t w0 = readfirstlane64(in_off);
-            const uint32_t lob = (uint32_t)((in_off - w0) * 4);
+            const uint32_t lob = (uint32_t)((in_off - w0) * EB);
             const T *wb = c.big + w0 + c.isw;              // uniform
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
@@ -364,16 +400,16 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             }
         } else {
             // 64 input rows of N contiguous values (slot 0 fastest), 16-B loads
-            // (4 per lane)
+            // (IT per lane)
             const T *big = c.big;
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
+            for (int it = 0; it < IT; ++it) {
                 const int q = chunk(it);
                 const int rw = q / CPR, ch = q % CPR;
                 const int64_t ro = __shfl(in_off, rw, 64);  // row rw's input offset (held by lane rw)
-                const vec_t<T, 4> v = vload<4, kNtLoad, true>(big + ro + 4 * ch);
+                const vec_t<T, VE> v = vload<VE, kNtLoad, true>(big + ro + VE * ch);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) rg[4 * it + k] = v[k];
+                for (int k = 0; k < VE; ++k) rg[VE * it + k] = v[k];
             }
         }
     };
@@ -427,10 +463,10 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     // against 6.3 ms unfused; 10.9 ms when issued after the prefetch, 6.9 ms
     // with the loads removed); loading them a whole tile ahead needed 128
     // VGPRs and was slower -- profiles/r04_belief_fusion_ab.txt
-    float lv[16];
+    T lv[16];
     auto load_lam = [&](int64_t to) {
         if constexpr (FORM == kChainBwd && DENSE) {
-            const float *lb = c.lam + to + (int64_t)slab_w() * c.d_slab + lane;
+            const T *lb = c.lam + to + (int64_t)slab_w() * c.d_slab + lane;
 #pragma unroll
             for (int e = 0; e < 16; ++e) lv[e] = gload(lb + (int64_t)slab_e(e) * c.d_slab);
         }
@@ -439,7 +475,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     // caller issued the tile's lam loads (one-run launches: before the next
     // tile's row loads, so waiting for lam leaves those in flight); 2 = check
     // c.bel at run time and load lam here (multi-run launches)
-    auto run_tile = [&](auto bmc, float (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
+    auto run_tile = [&](auto bmc, T (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
         constexpr int BM = decltype(bmc)::value;
         if constexpr (FORM == kChainBwd && DENSE && BM == 2) {
             if (c.bel) load_lam(tout);
@@ -447,11 +483,10 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         if constexpr (FORM == kChainBwd) {
             // rows through the image, then this lane's 16 entries (slots 4.. = w)
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
+            for (int it = 0; it < IT; ++it) {
                 const int q = chunk(it);
                 const int rw = q / CPR, ch = q % CPR;
-                *reinterpret_cast<vec_t<T, 4> *>(img + rw * ROWB + 16 * ch) =
-                    vec_t<T, 4>{t[4 * it], t[4 * it + 1], t[4 * it + 2], t[4 * it + 3]};
+                *reinterpret_cast<vec_t<T, VE> *>(img + rw * ROWB + 16 * ch) = pack_vec<T, VE>(t + VE * it);
             }
             lds_barrier();
             int fixed = 0;
@@ -459,15 +494,15 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             for (int p = 4; p < F; ++p) fixed += wdig(p) << p;
             // local index e: slot 0 = bit 3 ... slot 3 = bit 0; row position: slot p
             // at 2^p, so the lane's 16 entries are the 16 consecutive positions
-            // fixed .. fixed + 15 (e bit-reversed): four 16-B reads (lane stride
+            // fixed .. fixed + 15 (e bit-reversed): IT 16-B reads (lane stride
             // ROWB = 65 x 16 B: a quarter-wave covers all 64 banks once) instead
             // of sixteen 4-B reads, which share 16 banks 4-way
-            float u[16];
+            T u[16];
 #pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) {
-                const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4> *>(img + lane * ROWB + 4 * fixed + 16 * c4);
+            for (int c4 = 0; c4 < IT; ++c4) {
+                const vec_t<T, VE> v = *reinterpret_cast<const vec_t<T, VE> *>(img + lane * ROWB + EB * fixed + 16 * c4);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) u[4 * c4 + k] = v[k];
+                for (int k = 0; k < VE; ++k) u[VE * c4 + k] = v[k];
             }
 #pragma unroll
             for (int e = 0; e < 16; ++e)
@@ -478,7 +513,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         auto dig1 = [&](int e, int p) { return p < 4 ? (e >> (3 - p)) & 1 : wdig(p); };
         static_for<4>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            split_step<F, 1, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig1);
+            split_step<T, F, 1, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig1);
         });
         // exchange: entry (n-digits 0-3 = e, slots 4.. = w) -> xch[(w * 16 + e) * 64 + lane]
 #pragma unroll
@@ -497,30 +532,30 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         };
         static_for<F - 4>([&](auto jc) {
             constexpr int j = 4 + decltype(jc)::value;
-            split_step<F, 2, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig2);
+            split_step<T, F, 2, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig2);
         });
         // (no per-tile rescale: it is folded into the G tables, SplitState)
 #pragma unroll
         for (int e = 0; e < 16; ++e)
-            lmax = fmaxf(lmax, t[e]);                                          // entries are >= 0, never NaN
+            lmax = t[e] > lmax ? t[e] : lmax;                                  // entries are >= 0, never NaN
 
         if constexpr (FORM == kChainFwd) {
             // row position of entry e: w * 16 + e (slot 0 most significant)
 #pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4)
-                *reinterpret_cast<vec_t<T, 4> *>(img + lane * ROWB + 4 * (w * 16 + 4 * c4)) =
-                    vec_t<T, 4>{t[4 * c4], t[4 * c4 + 1], t[4 * c4 + 2], t[4 * c4 + 3]};
+            for (int c4 = 0; c4 < IT; ++c4)
+                *reinterpret_cast<vec_t<T, VE> *>(img + lane * ROWB + EB * (w * 16 + VE * c4)) =
+                    pack_vec<T, VE>(t + VE * c4);
             lds_barrier();
             // the 64 rows are one contiguous block of 64 * N entries (planner-checked):
             // 1 KiB per wave-instruction (chunk())
             T *out = c.out + (DENSE ? tout : __shfl(out_off, 0, 64));
             // (tiles are whole: the planner requires rest dim 0 to be a multiple of 64)
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
+            for (int it = 0; it < IT; ++it) {
                 const int q = chunk(it);                   // 16-B chunk within the block
                 const int rw = q / CPR, ch = q % CPR;
-                const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4> *>(img + rw * ROWB + 16 * ch);
-                vstore<4, kNtStore, true>(out + 4 * (int64_t)q, v);
+                const vec_t<T, VE> v = *reinterpret_cast<const vec_t<T, VE> *>(img + rw * ROWB + 16 * ch);
+                vstore<VE, kNtStore, true>(out + VE * (int64_t)q, v);
             }
         } else {
             // slab stores: entry e has n-digits 0-3 = (w << HB | h), slots 4.. = sc
@@ -539,26 +574,24 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                     // (p = lam * pi; acc = 0; acc += p for s = 0, 1, ...)
 #pragma unroll
                     for (int e = 0; e < 16; ++e)
-                        *reinterpret_cast<T *>(img + lane * ROWB + 4 * (wsl | slab_e(e))) = lv[e] * t[e];
+                        *reinterpret_cast<T *>(img + lane * ROWB + EB * (wsl | slab_e(e))) = lv[e] * t[e];
                     lds_barrier();
                     if (w == 0) {
                         T acc = T(0);
 #pragma unroll 4
-                        for (int c4 = 0; c4 < N / 4; ++c4) {
-                            const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4> *>(img + lane * ROWB + 16 * c4);
-                            acc = acc + v[0];
-                            acc = acc + v[1];
-                            acc = acc + v[2];
-                            acc = acc + v[3];
+                        for (int c4 = 0; c4 < N / VE; ++c4) {
+                            const vec_t<T, VE> v = *reinterpret_cast<const vec_t<T, VE> *>(img + lane * ROWB + 16 * c4);
+#pragma unroll
+                            for (int k = 0; k < VE; ++k) acc = acc + v[k];
                         }
                         store_n<T, 1, kNtStore, true>(c.bel + tout + lane, &acc);
-                        bmax = fmaxf(bmax, acc);
+                        bmax = acc > bmax ? acc : bmax;
                     }
                     lds_barrier();                         // the image is the next tile's again
                 }
             } else {
                 const int64_t w0 = readfirstlane64(out_off);
-                const uint32_t lob = (uint32_t)((out_off - w0) * 4);
+                const uint32_t lob = (uint32_t)((out_off - w0) * EB);
                 T *wb = c.out + w0 + c.osw;                // uniform
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
@@ -575,10 +608,10 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     int64_t vb = blockIdx.x;
     if (vb >= total_vblocks) return;
     setup(vb);
-    float rg[16];
+    T rg[16];
     int64_t in_off, out_off;
     int32_t gb[F];
-    if constexpr (!MULTI && FORM == kChainBwd) {
+    if constexpr (MODE != 2 && FORM == kChainBwd) {
         // one bucket, backward form: the next tile's loads are issued
         // (unconditionally: the last tile is re-read rather than branching, so
         // the wait counts stay static) before the current tile is computed (two
@@ -599,7 +632,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         auto loop = [&](auto belc) {
             constexpr bool BEL = decltype(belc)::value;
             while (true) {
-                float t[16];
+                T t[16];
 #pragma unroll
                 for (int e = 0; e < 16; ++e) t[e] = rg[e];
                 if constexpr (BEL) {
@@ -615,9 +648,8 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 if (vb >= total_vblocks) break;
             }
         };
-        if (DENSE && c.bel) loop(std::true_type{});
-        else loop(std::false_type{});
-    } else if constexpr (!MULTI) {
+        loop(std::integral_constant<bool, DENSE && MODE == 1>{});
+    } else if constexpr (MODE != 2) {
         // one bucket, forward form: the next tile's loads go into registers at
         // the top of a tile and, once the tile is done, into this lane's own
         // slots of the exchange table, where the next tile reads them back
@@ -631,7 +663,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         // Loads are issued unconditionally (the last tile is re-read rather
         // than branching) so the wait counts stay static
         const int64_t last = total_vblocks - 1;
-        float p[16];
+        T p[16];
         auto stage = [&]() {
 #pragma unroll
             for (int e = 0; e < 16; ++e) xch[(w * 16 + e) * 64 + lane] = p[e];
@@ -640,7 +672,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         issue(in_off, p);
         stage();
         while (true) {
-            float t[16];
+            T t[16];
 #pragma unroll
             for (int e = 0; e < 16; ++e) t[e] = xch[(w * 16 + e) * 64 + lane];
             const int64_t vbn = vb + gridDim.x;
@@ -654,7 +686,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         }
     } else {
         while (true) {
-            float t[16];
+            T t[16];
             decode(vb, in_off, out_off, gb);
             issue(in_off, t);
             run_tile(std::integral_constant<int, 2>{}, t, out_off, gb);
@@ -673,9 +705,11 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
 #ifndef BNPP_SPLIT_WAVES_PER_CU
 #define BNPP_SPLIT_WAVES_PER_CU 16     // resident waves per CU the persistent grid is sized for
 #endif
-template <int F, int FORM, int DEP, bool DENSE>
+template <typename T, int F, int FORM, int DEP, bool DENSE, bool BEL>
 static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_t stream) {
-    const size_t shm = kRedBytes + split_xch_bytes(F) + split_img_bytes(F) + (size_t)small_elems * sizeof(float);
+    constexpr int EB = sizeof(T);
+    constexpr int MODE1 = BEL ? 1 : 0;                    // one-run kernel of this key
+    const size_t shm = kRedBytes + split_xch_bytes(F, EB) + split_img_bytes(F, EB) + (size_t)small_elems * EB;
     // per device (a process may drive several): the 160-KiB LDS opt-in of
     // this instantiation and the CU count the persistent grid is sized for
     struct DevState {
@@ -691,10 +725,10 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     {
         std::lock_guard<std::mutex> g(ds.mu);
         if (!ds.done[dev]) {
-            ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP, DENSE, false>,
+            ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<T, F, FORM, DEP, DENSE, MODE1>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (ds.attr[dev] == hipSuccess)
-                ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<F, FORM, DEP, DENSE, true>,
+                ds.attr[dev] = hipFuncSetAttribute((const void *)chain_split_kernel<T, F, FORM, DEP, DENSE, 2>,
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (hipDeviceGetAttribute(&ds.cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
                 ds.cus[dev] <= 0)
@@ -707,23 +741,31 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     const int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
     const int64_t grid = a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
     if (a.n_desc == 1)
-        hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP, DENSE, false>), dim3((unsigned)grid),
+        hipLaunchKernelGGL((chain_split_kernel<T, F, FORM, DEP, DENSE, MODE1>), dim3((unsigned)grid),
                            dim3(64 * split_waves(F)), shm, stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
     else
-        hipLaunchKernelGGL((chain_split_kernel<F, FORM, DEP, DENSE, true>), dim3((unsigned)grid),
+        hipLaunchKernelGGL((chain_split_kernel<T, F, FORM, DEP, DENSE, 2>), dim3((unsigned)grid),
                            dim3(64 * split_waves(F)), shm, stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
     return hipGetLastError();
 }
 
 // forms kChainFwdS / kChainBwdS and their dense variants kChainFwdSD /
-// kChainBwdSD (bnpp_device.h), K = 2, F = 5..8, dep next / prev
-#define BNPP_CASE_CHAIN_SPLIT(F, FORM, KFORM, DEP, DENSE) \
-    case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F: return go_chain_split<F, KFORM, DEP, DENSE>(a, small_elems, stream);
-#define BNPP_CASE_CHAIN_SPLIT_OK(F, FORM, KFORM, DEP, DENSE) case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F: return true;
-#define BNPP_CHAIN_SPLIT_FD(X, F) X(F, 5, kChainFwd, 0, false) X(F, 5, kChainFwd, 1, false) \
-    X(F, 6, kChainBwd, 0, false) X(F, 6, kChainBwd, 1, false) X(F, 7, kChainFwd, 0, true) X(F, 7, kChainFwd, 1, true) \
-    X(F, 8, kChainBwd, 0, true) X(F, 8, kChainBwd, 1, true)
-#define BNPP_CHAIN_SPLIT(X) BNPP_CHAIN_SPLIT_FD(X, 5) BNPP_CHAIN_SPLIT_FD(X, 6) BNPP_CHAIN_SPLIT_FD(X, 7) \
-    BNPP_CHAIN_SPLIT_FD(X, 8)
+// kChainBwdSD (bnpp_device.h), K = 2, dep next / prev; F = 5..8 (fp32),
+// 5..7 (fp64); dense backward runs forming a fused belief have their own key
+// (chain_key + kChainBelKey)
+#define BNPP_CASE_CHAIN_SPLIT(T, F, FORM, KFORM, DEP, DENSE, BEL) \
+    case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F + (BEL ? kChainBelKey : 0): \
+        return go_chain_split<T, F, KFORM, DEP, DENSE, BEL>(a, small_elems, stream);
+#define BNPP_CASE_CHAIN_SPLIT_OK(T, F, FORM, KFORM, DEP, DENSE, BEL) \
+    case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F + (BEL ? kChainBelKey : 0): return true;
+#define BNPP_CHAIN_SPLIT_FD(X, T, F) X(T, F, 5, kChainFwd, 0, false, false) X(T, F, 5, kChainFwd, 1, false, false) \
+    X(T, F, 6, kChainBwd, 0, false, false) X(T, F, 6, kChainBwd, 1, false, false) \
+    X(T, F, 7, kChainFwd, 0, true, false) X(T, F, 7, kChainFwd, 1, true, false) \
+    X(T, F, 8, kChainBwd, 0, true, false) X(T, F, 8, kChainBwd, 1, true, false) \
+    X(T, F, 8, kChainBwd, 0, true, true) X(T, F, 8, kChainBwd, 1, true, true)
+#define BNPP_CHAIN_SPLIT(X) BNPP_CHAIN_SPLIT_FD(X, float, 5) BNPP_CHAIN_SPLIT_FD(X, float, 6) \
+    BNPP_CHAIN_SPLIT_FD(X, float, 7) BNPP_CHAIN_SPLIT_FD(X, float, 8)
+#define BNPP_CHAIN_SPLIT_F64(X) BNPP_CHAIN_SPLIT_FD(X, double, 5) BNPP_CHAIN_SPLIT_FD(X, double, 6) \
+    BNPP_CHAIN_SPLIT_FD(X, double, 7)
 
 }  // namespace bnpp

@@ -220,11 +220,12 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         if (cards[b.chain_x[j]] != K || (!sum && cards[b.chain_n[j]] != K)) return fail("chain: mixed cardinalities");
         N *= K;
     }
-    // split form (chainsplit.cuh): binary fp32 runs of 5..8 buckets over 2^(F-4) waves
+    // split form (chainsplit.cuh): binary runs of 5..8 (fp32) / 5..7 (fp64)
+    // buckets over 2^(F-4) waves
     const char *nsp = std::getenv("BNPP_NO_SPLIT");
     const char *smf = std::getenv("BNPP_SPLIT_MIN_F");
     const int split_min = smf ? std::max(5, std::atoi(smf)) : 5;
-    const bool split_ok = !(nsp && *nsp == '1') && K == 2 && eb == 4 && F >= split_min && F <= 8;
+    const bool split_ok = !(nsp && *nsp == '1') && K == 2 && F >= split_min && F <= split_max_f(eb);
     if ((N > 64 && !split_ok) || (K != 2 && K != 4)) return fail("chain: register table too large");
     std::vector<int> gidx(F, -1);                     // input index of G_j (-1: absent)
     int ni = 1;
@@ -363,7 +364,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         for (size_t q = 0; q < b.in[i].vars.size(); ++q) sp += (int64_t)(cards[b.in[i].vars[q]] - 1) * b.in[i].strides[q];
         g_pk += sp * kSplitPack;
     }
-    const bool pk_fits = g_pk * 4 <= split_g_budget_bytes(F);
+    const bool pk_fits = g_pk * eb <= split_g_budget_bytes(F, eb);
     if (chain_split_form(form) && (dep == kDepAny || !pk_fits)) {
         if (N > 64) return fail(pk_fits ? "chain: split form needs G_j to depend on one neighbouring slot"
                                         : "chain: packed G tables exceed the split form's LDS");
@@ -403,7 +404,8 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         // the belief (kChainBel): the dense backward form, the output's rest one
         // dense block below the slot stride S (belief entry r = output rest
         // offset), the forward message laid out exactly as the output
-        if (form != kChainBwdSD) return fail("chain: a fused belief needs the dense backward form");
+        if (form != kChainBwdSD || !chain_supported(eb, chain_key(form, K, F, dep) + kChainBelKey))
+            return fail("chain: a fused belief needs the dense backward form");
         const View &lam = b.in[ni];
         bool same = lam.vars.size() == b.out_vars.size() && rest == os[0];
         for (size_t i = 0; same && i < b.out_vars.size(); ++i) same = stride_of(lam, b.out_vars[i]) == ostr[i];
@@ -457,7 +459,7 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         d.in_base[ni] = b.in[ni].base;
     }
     d.small_elems = lo;
-    if ((int64_t)lo * eb > (chain_split_form(form) ? split_g_budget_bytes(F) : kStreamLdsBudget))
+    if ((int64_t)lo * eb > (chain_split_form(form) ? split_g_budget_bytes(F, eb) : kStreamLdsBudget))
         return fail("chain: G tables exceed the LDS budget");
     {
         uint32_t shift, magic;
@@ -866,7 +868,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
 }
 
 // ---------------------------------------------------------------- VE plan
-constexpr int kChainRunMax = 8;                   // longest fused run tried (split form: binary fp32)
+constexpr int kChainRunMax = 8;                   // longest fused run tried (split form: binary fp32; fp64: 7)
 // BNPP_CHAIN_RUN_MAX (tests): a shorter cap, to exercise the short-run kernels
 inline int chain_run_max() {
     const char *e = std::getenv("BNPP_CHAIN_RUN_MAX");
@@ -2471,7 +2473,8 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         }
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
-        it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf)
+        it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf) +
+                                  ((it.d.flags & kChainBel) ? kChainBelKey : 0)
                  : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes, it.d.slab_r)
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2)
                  : b.simple ? variant_key(kMaxIn, 1, 1)         // the widest input class runs any input count

@@ -369,6 +369,46 @@ def test_split_runs_identical_to_unfused(ctx, capfd, spec):
         assert _close(res[0][1][t], want[t], 1e-5), (t, res[0][1][t], want[t])
 
 
+@pytest.mark.parametrize("spec", [(16, 6, None, None), (18, 5, {3: 1, 40: 0}, None), (17, 4, None, 11)])
+def test_split_runs_fp64_identical_to_unfused(ctx, capfd, spec):
+    """fp64 split runs (chainsplit.cuh with T = double: runs of 5..7 buckets,
+    16 entries per lane, scalar fp64 arithmetic in the reference's order):
+    partition and tree marginals bit-identical to the one-thread runs, to one
+    bucket per launch, dense and general addressing alike; the last spec has
+    peaked potentials (every fused run rescales by 2^-50 or more).  The plan
+    holds F = 7 split runs (forms 7, 8 dense; 5, 6 general)."""
+    r, c, ev, log2_eps = spec
+    ev = ev or {}
+    d = synth.ising_grid(r, c, seed=13) if log2_eps is None else synth.peaked_grid(r, c, log2_eps=log2_eps, seed=5)
+    m = bnpp.Model.from_dict(d)
+    col = [i * c + j for j in range(c) for i in range(r)]
+    knobs = [{"BNPP_DEBUG_CHAIN": "1"}, {"BNPP_DEBUG_CHAIN": "1", "BNPP_NO_DENSE": "1"}, {"BNPP_NO_SPLIT": "1"},
+             {"BNPP_NO_CHAIN": "1"}]
+    res = []
+    for kn in knobs:
+        os.environ.update(kn)
+        os.environ["BNPP_TREE_SLOTS"] = "3"
+        capfd.readouterr()
+        try:
+            out = [bnpp.partition(ctx, m, ev, "mf", bnpp.F64, order=col)[0],
+                   bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64, order=col)[0]]
+            res.append(out)
+        finally:
+            for key in list(kn) + ["BNPP_TREE_SLOTS"]:
+                del os.environ[key]
+        if "BNPP_DEBUG_CHAIN" in kn:
+            err = capfd.readouterr().err
+            forms = (5, 6) if "BNPP_NO_DENSE" in kn else (7, 8)
+            assert any("run form %d K=2 F=7" % f in err for f in forms), err[-2000:]
+    for out in res[1:]:
+        assert out == res[0]
+    want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    for t in range(m.n_vars):
+        assert _close(res[0][1][t], want[t], 1e-12), (t, res[0][1][t], want[t])
+    rz, _ = refcpu.Model.from_dict(d).partition(ev, "mf")
+    assert abs(res[0][0] - math.log10(rz)) <= 1e-12 * abs(math.log10(rz)), (res[0][0], math.log10(rz))
+
+
 def _bucket_max_log2(d, rows, cols):
     """max over x of the product of the column-sweep bucket of each variable
     above the last row (unary, right pair, down pair), as log2"""
@@ -476,8 +516,9 @@ def _two_grids(a, b):
             "scopes": a["scopes"] + [[v + n for v in s] for s in b["scopes"]], "values": a["values"] + b["values"]}
 
 
-@pytest.mark.parametrize("model", ["ising", "peaked", "two"])
-def test_fused_beliefs_identical_to_belief_passes(ctx, capfd, model):
+@pytest.mark.parametrize("model,dt", [("ising", "f32"), ("peaked", "f32"), ("two", "f32"), ("ising", "f64"),
+                                      ("peaked", "f64")])
+def test_fused_beliefs_identical_to_belief_passes(ctx, capfd, model, dt):
     """Deliveries whose belief sums the slots of the backward run that made
     its message (kChainBel: 16x6 column sweeps with 2^8-entry kept sets, so a
     belief sums 8 binary variables) are formed inside that run -- it also
@@ -487,7 +528,11 @@ def test_fused_beliefs_identical_to_belief_passes(ctx, capfd, model):
     marginals are bit-identical to the separate belief passes
     (BNPP_NO_BEL_FUSE), to one-thread runs and to one bucket per launch, and
     within fp32 rounding of the fp64 per-target engine; peaked potentials
-    (every bucket product <= 2^-10) and two disconnected grids included."""
+    (every bucket product <= 2^-10) and two disconnected grids included.
+    fp64: split runs of 7 buckets, 2^7-entry kept sets (a belief sums 7
+    variables), the fp64 belief kernel; within 1e-12 of the per-target engine."""
+    dtype = bnpp.F32 if dt == "f32" else bnpp.F64
+    keep = "8" if dt == "f32" else "7"
     if model == "ising":
         d = synth.ising_grid(16, 6, seed=31)
     elif model == "peaked":
@@ -501,10 +546,10 @@ def test_fused_beliefs_identical_to_belief_passes(ctx, capfd, model):
     res = []
     for kn in knobs:
         os.environ.update(kn)
-        os.environ.update({"BNPP_KEEP_LOG2": "8", "BNPP_TREE_SLOTS": "3"})
+        os.environ.update({"BNPP_KEEP_LOG2": keep, "BNPP_TREE_SLOTS": "3"})
         capfd.readouterr()
         try:
-            res.append(bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F32, order=order)[0])
+            res.append(bnpp.marginals_tree(ctx, m, {}, "mf", dtype, order=order)[0])
         finally:
             for key in list(kn) + ["BNPP_KEEP_LOG2", "BNPP_TREE_SLOTS"]:
                 del os.environ[key]
@@ -514,8 +559,9 @@ def test_fused_beliefs_identical_to_belief_passes(ctx, capfd, model):
     for out in res[1:]:
         assert out == res[0]
     want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
+    tol = 1e-5 if dt == "f32" else 1e-12
     for t in range(m.n_vars):
-        assert _close(res[0][t], want[t], 1e-5), (t, res[0][t], want[t])
+        assert _close(res[0][t], want[t], tol), (t, res[0][t], want[t])
 
 
 @pytest.mark.parametrize("n_parts", [2, 3])
