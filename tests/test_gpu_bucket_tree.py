@@ -529,10 +529,10 @@ def test_fused_beliefs_identical_to_belief_passes(ctx, capfd, model, dt):
     (BNPP_NO_BEL_FUSE), to one-thread runs and to one bucket per launch, and
     within fp32 rounding of the fp64 per-target engine; peaked potentials
     (every bucket product <= 2^-10) and two disconnected grids included.
-    fp64: split runs of 7 buckets, 2^7-entry kept sets (a belief sums 7
+    fp64: split runs of 7 buckets, 2^9-entry kept sets (a belief sums 7
     variables), the fp64 belief kernel; within 1e-12 of the per-target engine."""
     dtype = bnpp.F32 if dt == "f32" else bnpp.F64
-    keep = "8" if dt == "f32" else "7"
+    keep = "8" if dt == "f32" else "9"
     if model == "ising":
         d = synth.ising_grid(16, 6, seed=31)
     elif model == "peaked":
