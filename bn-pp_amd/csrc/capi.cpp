@@ -335,7 +335,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             std::string msg;
             VEPlan cp;
             if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), part, n_parts, cp, &msg, chain_eb,
-                                        n_slices, slice_rank))
+                                        n_slices, slice_rank, false, eb))
                 return set_err(BNPP_ERR_UNSUPPORTED, msg);
             plans.back() = std::move(cp);
         } else if (need(plans.back()) > budget || n_parts > 1 || n_slices > 1) {
@@ -348,7 +348,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             if (n_slices > 1 && !(std::getenv("BNPP_SLICE_LANES") && *std::getenv("BNPP_SLICE_LANES") == '0')) {
                 VEPlan cp;
                 if (plan_bucket_tree_chain(d.cards, views, ord, targets, 1, part, n_parts, cp, &msg, chain_eb, n_slices,
-                                           slice_rank, true)) {
+                                           slice_rank, true, eb)) {
                     if (need(cp) <= budget) {
                         plans.back() = std::move(cp);
                         return BNPP_OK;
@@ -369,7 +369,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             if (memo_s > 0) {                             // the search would land on the same count
                 VEPlan cp;
                 if (plan_bucket_tree_chain(d.cards, views, ord, targets, memo_s, part, n_parts, cp, &msg, chain_eb, n_slices,
-                                           slice_rank) &&
+                                           slice_rank, false, eb) &&
                     need(cp) <= budget) {
                     best_s = memo_s;
                     best = std::move(cp);
@@ -391,7 +391,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                 std::vector<std::string> msgs(n);
                 parallel_for((int64_t)n, [&](int64_t i) {
                     planned[i] = plan_bucket_tree_chain(d.cards, views, ord, targets, probe[i], part, n_parts, cps[i],
-                                                        &msgs[i], chain_eb, n_slices, slice_rank) ? 1 : 0;
+                                                        &msgs[i], chain_eb, n_slices, slice_rank, false, eb) ? 1 : 0;
                     if (planned[i]) nb[i] = need(cps[i]);
                 });
                 int new_lo = lo, new_hi = hi;

@@ -893,7 +893,7 @@ struct PlanBuilder {
     std::vector<int> rank;
     std::vector<int> level;                 // per table
     bool sequential = false;                // every bucket one level after the previous (program order)
-    // reductions of a delivered kept table (<= 2^24 entries, read once each):
+    // reductions of a delivered kept table (<= 2^25 entries, read once each):
     // placed one level after their own input (and after free_base, the level
     // the delivery's reductions start from), not in program order, so the
     // reductions at one depth of a delivery's tree share a level and a launch
@@ -950,7 +950,7 @@ struct PlanBuilder {
         b.elim_var = x;
         b.out_vars = ov;
         b.out_table = new_msg(ov);
-        const bool small = free_small && table_size(ov, cards) <= ((int64_t)1 << 24);
+        const bool small = free_small && table_size(ov, cards) <= ((int64_t)1 << 25);
         int lv = sequential && !free_level ? (small ? free_base : last_level) : 0;
         for (const View &v : in) lv = std::max(lv, level[v.table]);
         b.level = lv + 1;
@@ -1124,8 +1124,12 @@ struct PlanBuilder {
         const int F = (int)b.chain_n.size();
         if (b.chain_x.empty() || b.bel_table >= 0 || b.out_table != pi.table || pi.base != 0 || lam.base != 0 ||
             (int)slow.size() != F || (int)pi.vars.size() <= F || lam.vars != pi.vars || lam.strides != pi.strides ||
-            lam.table < p.n_src || level[lam.table] >= b.level)
+            lam.table < p.n_src || level[lam.table] >= b.level) {
+            if (std::getenv("BNPP_DEBUG_CHAIN"))
+                std::fprintf(stderr, "[chain] belief not fused: run F=%d (out %d, pi %d), %zu slow variables\n", F,
+                             b.out_table, pi.table, slow.size());
             return -1;
+        }
         for (int i = 0; i < F; ++i)
             if (!contains(slow, pi.vars[i]) || !contains(b.chain_n, pi.vars[i])) return -1;
         const std::vector<int> kv(pi.vars.begin() + F, pi.vars.end());
@@ -1432,7 +1436,7 @@ int64_t binom_capped(int n, int k) {             // C(n, k), saturating at 2^40
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
                             int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb, int n_slices,
-                            int slice_rank, bool lanes) {
+                            int slice_rank, bool lanes, int elem_bytes) {
     if (n_parts < 1 || part < 0 || part >= n_parts) {
         if (msg) *msg = "bad part";
         return false;
@@ -1504,10 +1508,15 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
     // positions, and the forward messages are only recomputed to reach those.
     // 2^24 kept entries (measured on the 32x32 column sweep: 2^21 -> 2^24 cuts
     // the plan from 14.6 to 13.3 TB and the MAR from 2.96 to 2.73 s; kept sets
-    // matter only for separators above 2^24 entries).  BNPP_KEEP_LOG2 /
-    // BNPP_SLOW_LOG2 override them (tests use tiny values on small grids).
+    // matter only for separators above 2^24 entries); fp64: 2^25, so a
+    // 32-wide separator's belief sums 7 variables, the longest fp64 split run
+    // (a delivery's belief is formed inside the backward run that ends there
+    // when that run's slots are the summed variables, attach_belief).
+    // BNPP_KEEP_LOG2 / BNPP_SLOW_LOG2 override them (tests use tiny values on
+    // small grids).
     const char *ke = std::getenv("BNPP_KEEP_LOG2"), *se = std::getenv("BNPP_SLOW_LOG2");
-    const int64_t kKeepMax = (int64_t)1 << (ke ? std::atoi(ke) : 24), kSlowMax = (int64_t)1 << (se ? std::atoi(se) : 13);
+    const int64_t kKeepMax = (int64_t)1 << (ke ? std::atoi(ke) : elem_bytes == 8 ? 25 : 24),
+                  kSlowMax = (int64_t)1 << (se ? std::atoi(se) : 13);
     auto slow_part = [&](const std::vector<int> &sep) {     // slowest vars summed in the first pass
         std::vector<int> slow;
         int64_t P = 1;
@@ -1724,7 +1733,10 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             }
             have_pi = true;
         };
-        auto pi_down_to = [&](int j) {
+        // last: the length the run ending at j should have (a delivery's
+        // belief fuses into that run only when its slots are exactly the
+        // belief's summed variables, attach_belief); 0: any partition
+        auto pi_down_to = [&](int j, int last = 0) {
             int jj = pi_pos - 1;
             while (jj >= j) {
                 // buckets jj+1, jj, ... of one slicing window (a run may not cross an exchange)
@@ -1732,7 +1744,11 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 while (jj - span >= j && win[jj + 1 - span] == win[jj + 1]) ++span;
                 // longest fusable run of backward buckets jj, jj-1, ... (chain.cuh)
                 int fused = 0;
-                for (int F = chain_first_try(span); F >= 2 && have_pi && !fused; --F) {
+                int first = chain_first_try(span);
+                const int rem = jj - j + 1;                       // buckets left down to j
+                if (last >= 2 && rem > last) first = std::min(first, rem - last);
+                else if (last >= 2 && rem == last) first = std::min(first, last);
+                for (int F = first; F >= 2 && have_pi && !fused; --F) {
                     if (span - F == 1 && F > 2) continue;   // never strand one bucket
                     std::vector<PlanBuilder::ChainStep> steps;
                     std::vector<int> vars = pi_cur.vars;
@@ -1804,7 +1820,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                     // where they are small beside the messages -- a kept table of
                     // <= 1/64 of the largest -- else the arena would grow)
                     const int64_t kt = B.p.msgs[tb - B.p.n_src].size;
-                    B.free_small = !(nf && *nf == '1') && kt <= ((int64_t)1 << 24) && kt * 64 <= B.p.max_table;
+                    B.free_small = !(nf && *nf == '1') && kt <= ((int64_t)1 << 25) && kt * 64 <= B.p.max_table;
                     B.free_base = B.last_level;
                     B.reduce_many(B.view(tb), mit->second, result_of);
                     B.free_small = false;
@@ -1819,10 +1835,16 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 for (int t : dit->second) result_of[t] = B.reduce_to(bel, t);
             }
         };
+        // the run length that lets delivery j's belief fuse (attach_belief)
+        auto bel_run = [&](int j) {
+            if (sbits != 0 || !multi.count(j) || B.chain_eb == 0) return 0;
+            const int f = (int)slow[j].size();
+            return f >= 5 && f <= split_max_f(B.chain_eb) ? f : 0;
+        };
         auto deliver = [&](int i, const View &lam_j) {
             if (i != next_deliver) return false;
             const int j = D[i];
-            pi_down_to(j);
+            pi_down_to(j, bel_run(j));
             std::vector<View> bel{lam_j};
             if (have_pi) bel.push_back(pi_cur);
             deliver_bel(j, bel);

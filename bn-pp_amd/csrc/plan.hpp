@@ -190,10 +190,11 @@ VEPlan plan_bucket_tree(const std::vector<int> &cards, const std::vector<View> &
 // marginal of every target: the marginals are the sum over ranks.  lanes:
 // the two-front schedule (forward and backward messages on two concurrent
 // lanes, no recomputation; `slots` unused), else binomial checkpointing.
+// elem_bytes: the dtype's (the kept-set size of a delivery depends on it).
 bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<View> &sources,
                             const std::vector<int> &order, const std::vector<int> &targets, int slots,
                             int part, int n_parts, VEPlan &out, std::string *msg, int chain_eb = 0,
-                            int n_slices = 1, int slice_rank = 0, bool lanes = false);
+                            int n_slices = 1, int slice_rank = 0, bool lanes = false, int elem_bytes = 4);
 
 // Flattened, level-ordered launch schedule over one or more plans sharing the
 // same sources.  Tables: [0, n_src) sources, then every plan's messages.
