@@ -28,7 +28,7 @@
 
 using namespace bnpp;
 
-constexpr int kTimingPhases = 11;
+constexpr int kTimingPhases = 9;
 
 struct bnpp_ctx {
     Context c;
@@ -854,7 +854,6 @@ int oneshot_job(bnpp_ctx *ctx, bool cache_ok, uint64_t key, Create &&create, bnp
         for (int i = 0; i < 3; ++i) g_timing[i] = 0;
         g_timing[7] = 1;
         g_timing[8] = 0;
-        g_timing[9] = g_timing[10] = 0;
         return BNPP_OK;
     }
     std::unique_ptr<bnpp_job> j;
@@ -876,13 +875,6 @@ void oneshot_done(bnpp_ctx *ctx, bool cache_ok, uint64_t key, bnpp_job *job, int
 }
 
 // launch / run+fetch / free / total of a call whose create_job filled phases 0-2
-// the arena's mapping during the job's last launch (VMM arenas,
-// runtime.cpp VmmArena): all of it, and the part before the first level
-void record_map_timing(const bnpp_job *job) {
-    g_timing[9] = job ? job->pg.vmm_map_ms : 0.0;
-    g_timing[10] = job ? job->pg.vmm_first_ms : 0.0;
-}
-
 void record_call_timing(double t0, double t1, double t2, double t3) {
     g_timing[3] = t2 - t1;
     g_timing[4] = t3 - t2;
@@ -1395,7 +1387,6 @@ int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     double lz = 0, zz = 0;
     if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, &lz, &zz);
     const double t3 = now_ms();
-    record_map_timing(job);
     oneshot_done(ctx, cache_ok, key, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (rc) return rc;
@@ -1426,7 +1417,6 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     const double t2 = now_ms();
     if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, out, nullptr);
     const double t3 = now_ms();
-    record_map_timing(job);
     oneshot_done(ctx, cache_ok, key, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (std::getenv("BNPP_TIMING"))
@@ -1467,7 +1457,6 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
     const double t2 = now_ms();
     if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, out, nullptr, owned);
     const double t3 = now_ms();
-    record_map_timing(job);
     oneshot_done(ctx, cache_ok, key, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (timing)
@@ -1501,7 +1490,6 @@ int bnpp_marginals_tree_sliced(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, con
     const double t2 = now_ms();
     if (rc == BNPP_OK) rc = job_results_sliced(job.get(), ctx->c.stream, out, out_exp2);
     const double t3 = now_ms();
-    record_map_timing(job.get());
     if (job) destroy_job(job.release());
     record_call_timing(t0, t1, t2, t3);
     if (std::getenv("BNPP_TIMING"))

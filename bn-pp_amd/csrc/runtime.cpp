@@ -2,9 +2,6 @@
 #include <chrono>
 #include "runtime.hpp"
 
-#include <climits>
-#include <cstdlib>
-
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -24,88 +21,7 @@ uint64_t bits_of(T x) {
     return b;
 }
 
-double ms_since(std::chrono::steady_clock::time_point t0) {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-}
-
-hipMemAllocationProp vmm_prop(int device) {
-    hipMemAllocationProp prop = {};
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = device;
-    return prop;
-}
-
 }  // namespace
-
-// ------------------------------------------------------------ VMM arena
-bool vmm_reserve(int device, size_t bytes, VmmArena &a) {
-    int ok = 0;
-    if (hipDeviceGetAttribute(&ok, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !ok)
-        return false;
-    hipMemAllocationProp prop = vmm_prop(device);
-    size_t g = 0;
-    if (hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || g == 0)
-        return false;
-    // 2-GiB chunks: a 258-GB arena is ~120 of them (0.2-0.3 ms each to map),
-    // fine enough that a level waits only for the chunks it touches
-    const size_t chunk = (((size_t)2 << 30) + g - 1) / g * g;
-    const size_t n = (std::max<size_t>(bytes, 1) + chunk - 1) / chunk;
-    void *base = nullptr;
-    if (hipMemAddressReserve(&base, n * chunk, 0, nullptr, 0) != hipSuccess || !base) return false;
-    a.base = base;
-    a.bytes = n * chunk;
-    a.chunk = chunk;
-    a.device = device;
-    a.handles.assign(n, hipMemGenericAllocationHandle_t{});
-    a.created.assign(n, 0);
-    return true;
-}
-
-void vmm_set_order(VmmArena &a, std::vector<int> order) {
-    const int n = (int)a.handles.size();
-    std::vector<char> seen(n, 0);
-    for (int c : order) seen[c] = 1;
-    for (int c = 0; c < n; ++c)
-        if (!seen[c]) order.push_back(c);
-    a.order = std::move(order);
-}
-
-hipError_t vmm_map_to(VmmArena &a, int prefix, double *ms) {
-    if (a.mapped >= prefix) return hipSuccess;
-    const auto t0 = std::chrono::steady_clock::now();
-    const hipMemAllocationProp prop = vmm_prop(a.device);
-    hipMemAccessDesc acc = {};
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    hipError_t e = hipSuccess;
-    for (; a.mapped < prefix && a.mapped < (int)a.order.size(); ++a.mapped) {
-        const int c = a.order[a.mapped];
-        void *p = static_cast<unsigned char *>(a.base) + (size_t)c * a.chunk;
-        // the driver hands out HBM cleared: this is where a chunk waits for
-        // the clearing of memory freed shortly before
-        if ((e = hipMemCreate(&a.handles[c], a.chunk, &prop, 0)) != hipSuccess) break;
-        a.created[c] = 1;
-        if ((e = hipMemMap(p, a.chunk, 0, a.handles[c], 0)) != hipSuccess) break;
-        a.created[c] = 2;
-        if ((e = hipMemSetAccess(p, a.chunk, &acc, 1)) != hipSuccess) break;
-    }
-    if (ms) *ms += ms_since(t0);
-    return e;
-}
-
-void vmm_release(VmmArena &a) {
-    (void)hipSetDevice(a.device);
-    for (size_t c = 0; c < a.handles.size(); ++c) {
-        void *p = static_cast<unsigned char *>(a.base) + c * a.chunk;
-        if (a.created[c] == 2) (void)hipMemUnmap(p, a.chunk);
-        if (a.created[c] >= 1) (void)hipMemRelease(a.handles[c]);
-        a.created[c] = 0;
-    }
-    if (a.base) (void)hipMemAddressFree(a.base, a.bytes);
-    a.base = nullptr;
-    a.bytes = 0;
-}
 
 hipError_t get_buffer(Context &ctx, size_t bytes, void **p, size_t *cap) {
     bytes = bytes ? bytes : 256;
@@ -334,8 +250,7 @@ static int run_xchg(Context &ctx, Executable &ex, const Schedule::Group &g, hipS
     return 0;
 }
 
-int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks, VmmArena *vmm,
-           const std::vector<int> *need, double *map_ms, double *first_ms) {
+int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks) {
     const Schedule &sc = ex.sched;
     hipError_t err = hipMemcpyAsync(ex.d_meta, ex.d_meta0, sizeof(TableMeta) * (size_t)sc.n_tables,
                                     hipMemcpyDeviceToDevice, stream);
@@ -348,11 +263,6 @@ int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *ho
     for (size_t gi = 0; gi < sc.groups.size(); ++gi) {
         const Schedule::Group &g = sc.groups[gi];
         hipStream_t st = ls[lanes ? g.lane & 1 : 0];
-        // a VMM arena not fully mapped: the group's chunks are mapped before
-        // it is enqueued (the device keeps running the levels before it)
-        if (vmm && need && gi < need->size() &&
-            (err = vmm_map_to(*vmm, (*need)[gi], gi == 0 ? first_ms : map_ms)) != hipSuccess)
-            return fail(ctx, err, "arena mapping (hipMemCreate / hipMemMap)");
         if (lanes)
             for (int e : ex.g_wait[gi])
                 if ((err = hipStreamWaitEvent(st, ex.events[e], 0)) != hipSuccess) return fail(ctx, err, "lane wait");
@@ -422,66 +332,10 @@ void free_executable(Context &ctx, Executable &ex) {
 }
 
 void drop_arena_cache(Context &ctx) {
-    if (ctx.arena_cache_vmm) ctx.arena_cache_vmm.reset();       // the last owner releases it
-    else if (ctx.arena_cache) (void)hipFree(ctx.arena_cache);
+    if (ctx.arena_cache) (void)hipFree(ctx.arena_cache);
     ctx.arena_cache = nullptr;
     ctx.arena_cache_bytes = 0;
 }
-
-namespace {
-
-// VMM arenas from this size up (smaller ones map at once, nothing to hide);
-// BNPP_NO_VMM=1 keeps one hipMalloc (A/B, and the tests' comparison)
-bool use_vmm(int64_t need) {
-    const char *e = std::getenv("BNPP_NO_VMM");
-    return !(e && *e == '1') && need >= ((int64_t)8 << 30);
-}
-
-// Mapping order of a VMM arena's chunks and, per part and group, how many of
-// them (a prefix of the order) must be mapped before the group is enqueued:
-// chunks ordered by the first group (parts in order) that reads or writes a
-// table in them.
-void vmm_plan(const Program &pg, int64_t eb, std::vector<int> &order, std::vector<std::vector<int>> &need) {
-    const VmmArena &a = *pg.vmm;
-    const int n = (int)a.handles.size();
-    const int64_t kNever = INT64_MAX;
-    std::vector<int64_t> first(n, kNever);
-    int64_t gidx = 0;
-    for (const Executable &ex : pg.parts) {
-        const Schedule &sc = ex.sched;
-        auto touch = [&](int t) {
-            if (t < sc.n_src || t >= sc.n_tables) return;
-            const int64_t lo = sc.table_offset[t], hi = lo + std::max<int64_t>(sc.table_size[t], 1) * eb;
-            for (int64_t c = lo / (int64_t)a.chunk; c <= (hi - 1) / (int64_t)a.chunk && c < n; ++c)
-                first[c] = std::min(first[c], gidx);
-        };
-        for (const Schedule::Group &g : sc.groups) {
-            for (int k = g.begin; k < g.end; ++k) {
-                const BucketDesc &d = sc.descs[k];
-                const int n_read = d.n_in + ((d.flags & kChainBel) ? 1 : 0);
-                for (int i = 0; i < n_read && i < kMaxDescIn; ++i) touch(d.in_table[i]);
-                touch(d.out_table);
-                if (d.flags & kChainBel) touch(d.aux_out);
-            }
-            ++gidx;
-        }
-    }
-    order.clear();
-    for (int c = 0; c < n; ++c)
-        if (first[c] != kNever) order.push_back(c);
-    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return first[x] < first[y]; });
-    need.assign(pg.parts.size(), {});
-    gidx = 0;
-    size_t k = 0;
-    for (size_t b = 0; b < pg.parts.size(); ++b) {
-        for (size_t gi = 0; gi < pg.parts[b].sched.groups.size(); ++gi, ++gidx) {
-            while (k < order.size() && first[order[k]] <= gidx) ++k;
-            need[b].push_back((int)k);
-        }
-    }
-}
-
-}  // namespace
 
 int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg,
                  bool use_cache) {
@@ -492,48 +346,23 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
     hipError_t err = hipSetDevice(ctx.device);
     if (err != hipSuccess) return fail(ctx, err, "hipSetDevice");
     const int64_t need = std::max<int64_t>(pg.arena_bytes, 256);
-    if (use_cache && ctx.arena_cache && ctx.arena_cache_bytes >= need && ctx.arena_cache_vmm &&
-        ctx.arena_cache_vmm->mapped < (int)ctx.arena_cache_vmm->handles.size())
-        drop_arena_cache(ctx);                           // an earlier call failed to map it all
     if (use_cache && ctx.arena_cache && ctx.arena_cache_bytes >= need) {
         pg.arena = ctx.arena_cache;
-        pg.vmm = ctx.arena_cache_vmm;
         pg.arena_cached = true;
         pg.arena_reused = true;
     } else {
         if (use_cache) drop_arena_cache(ctx);            // too small: replace it
-        // the plan's own size (not the budget).  A hipMalloc here is where a
+        // the plan's own size (not the budget).  This hipMalloc is where a
         // cold call waits for the driver to clear HBM another process (or
         // this one) freed shortly before -- ~36 GB/s of backlog, one wait
         // whatever the size asked (tools/map_probe.hip,
-        // profiles/r04_map_probe.log) -- so it is timed on its own.  Large
-        // arenas are reserved instead and mapped by a helper while the run
-        // goes (VmmArena); the reservation is what is timed then
+        // profiles/r04_map_probe.log) -- so it is timed on its own
         const auto ta = std::chrono::steady_clock::now();
-        std::shared_ptr<VmmArena> v;
-        if (use_vmm(need)) {
-            // released by its last owner (the program, or the context's cache)
-            v = std::shared_ptr<VmmArena>(new VmmArena, [](VmmArena *a) {
-                if (a->base) {
-                    (void)hipSetDevice(a->device);
-                    (void)hipDeviceSynchronize();          // nothing may still run in it
-                }
-                vmm_release(*a);
-                delete a;
-            });
-            if (!vmm_reserve(ctx.device, (size_t)need, *v)) v.reset();
-        }
-        if (v) {
-            pg.arena = v->base;
-            pg.vmm = v;
-        } else if ((err = hipMalloc(&pg.arena, (size_t)need)) != hipSuccess) {
-            return fail(ctx, err, "hipMalloc(arena)");
-        }
-        pg.arena_alloc_ms = ms_since(ta);
+        if ((err = hipMalloc(&pg.arena, (size_t)need)) != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
+        pg.arena_alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
         if (use_cache) {
             ctx.arena_cache = pg.arena;
             ctx.arena_cache_bytes = need;
-            ctx.arena_cache_vmm = pg.vmm;
             pg.arena_cached = true;
         }
     }
@@ -580,38 +409,20 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
                 return fail(ctx, err, "hipMemcpy(copies)");
         }
     }
-    // a new VMM arena: chunks mapped by the launch as levels first need them
-    if (pg.vmm && !pg.arena_reused) {
-        std::vector<int> order;
-        vmm_plan(pg, eb, order, pg.vmm_need);
-        vmm_set_order(*pg.vmm, std::move(order));
-        pg.vmm_pending = true;
-    }
     return 0;
 }
 
 int launch_program(Context &ctx, Program &pg, hipStream_t stream) {
     const int64_t eb = pg.dtype == kF32 ? 4 : 8;
     (void)eb;
-    pg.vmm_map_ms = pg.vmm_first_ms = 0;
-    VmmArena *vmm = pg.vmm_pending ? pg.vmm.get() : nullptr;
     for (size_t b = 0; b < pg.parts.size(); ++b) {
         Executable &ex = pg.parts[b];
-        int rc = launch(ctx, ex, stream, &pg.hooks, vmm, vmm ? &pg.vmm_need[b] : nullptr, &pg.vmm_map_ms,
-                        b == 0 ? &pg.vmm_first_ms : &pg.vmm_map_ms);
+        int rc = launch(ctx, ex, stream, &pg.hooks);
         if (rc) return rc;
         if (ex.n_copies > 0) {
             hipError_t err = launch_copies(ex.d_copies, ex.n_copies, ex.copy_max_bytes, stream);
             if (err != hipSuccess) return fail(ctx, err, "launch_copies");
         }
-    }
-    if (vmm) {
-        // the rest of the range (chunks no level touched): later launches of
-        // this program, and later programs in the cached arena, map nothing
-        hipError_t err = vmm_map_to(*vmm, (int)vmm->handles.size(), &pg.vmm_map_ms);
-        if (err != hipSuccess) return fail(ctx, err, "arena mapping (hipMemCreate / hipMemMap)");
-        pg.vmm_map_ms += pg.vmm_first_ms;
-        pg.vmm_pending = false;
     }
     return 0;
 }
@@ -660,8 +471,7 @@ int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std
 
 void free_program(Context &ctx, Program &pg) {
     for (Executable &ex : pg.parts) free_executable(ctx, ex);
-    if (pg.arena && !pg.arena_cached && !pg.vmm) (void)hipFree(pg.arena);
-    pg.vmm.reset();                                  // a VMM arena: released by its last owner
+    if (pg.arena && !pg.arena_cached) (void)hipFree(pg.arena);
     put_buffer(ctx, pg.results, pg.results_cap);
     pg = Program{};
 }

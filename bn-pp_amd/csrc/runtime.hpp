@@ -3,7 +3,6 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
-#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -69,35 +68,6 @@ hipError_t launch_bp_flood_marginals(const BpFlood &a, hipStream_t stream);
 
 enum DType { kF64 = 0, kF32 = 1 };
 
-// An arena reserved as one virtual range and backed chunk by chunk (HIP's
-// virtual-memory API) as the launch loop reaches the first level that touches
-// each chunk.  A cold call's hipMalloc of the whole arena waited for the
-// driver to clear HBM that any process freed shortly before (~36 GB/s of
-// backlog, profiles/r04_map_probe.log) before the first kernel could run;
-// mapped on demand, a chunk waits only for its own share of that backlog,
-// while the device runs the levels already enqueued before it.  The mapping
-// is done by the launching thread itself: a helper thread mapping
-// concurrently blocked the launch loop anyway (kernel code objects load on
-// first launch and wait behind the helper's allocation: profiles/r05_vmm_helper.log).
-struct VmmArena {
-    void *base = nullptr;
-    size_t bytes = 0;                  // reserved (a multiple of `chunk`)
-    size_t chunk = 0;
-    int device = 0;
-    std::vector<hipMemGenericAllocationHandle_t> handles;   // per chunk, once created
-    std::vector<char> created;         // 0 none, 1 created, 2 mapped
-    std::vector<int> order;            // chunks in mapping order
-    int mapped = 0;                    // prefix of `order` mapped and accessible
-};
-// reserve `bytes` of address space; false when the device has no VMM support
-bool vmm_reserve(int device, size_t bytes, VmmArena &a);
-// the mapping order (chunks missing from `order` go last)
-void vmm_set_order(VmmArena &a, std::vector<int> order);
-// map the chunks of the order up to `prefix`; adds the time spent to *ms
-hipError_t vmm_map_to(VmmArena &a, int prefix, double *ms);
-// unmap and release every chunk, free the range
-void vmm_release(VmmArena &a);
-
 struct Context {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -108,7 +78,6 @@ struct Context {
     // allocator the context holds on to it until it is destroyed
     void *arena_cache = nullptr;
     int64_t arena_cache_bytes = 0;
-    std::shared_ptr<VmmArena> arena_cache_vmm;          // when the cached arena is VMM-backed
     // small device buffers (sources, descriptors, dims pool, metadata, results)
     // kept for reuse: a one-shot call otherwise pays ~10 hipMalloc / hipFree
     // pairs (hipFree synchronises), several ms of a small model's PR
@@ -176,12 +145,6 @@ struct Program {
     bool arena_cached = false;          // arena is the context's cache (not freed with the program)
     bool arena_reused = false;          // ... and was already allocated before this program
     double arena_alloc_ms = 0;          // hipMalloc of the arena (0 when reused), incl. the driver's HBM clearing wait
-                                        // (VMM arenas: the address reservation only)
-    std::shared_ptr<VmmArena> vmm;      // VMM-backed arena (owned here, or shared with the context's cache)
-    std::vector<std::vector<int>> vmm_need;   // per part, per group: chunks of vmm->order it touches by then
-    bool vmm_pending = false;           // chunks still unmapped: the launch maps them as levels need them
-    double vmm_map_ms = 0;              // last launch: time mapping chunks between levels (device busy meanwhile)
-    double vmm_first_ms = 0;            // ... of which before the first level (exposed)
     void *results = nullptr;
     size_t results_cap = 0;
     int64_t results_bytes = 0;
@@ -193,12 +156,7 @@ struct Program {
 int upload_sources(Context &ctx, const std::vector<std::vector<double>> &values, DType dt, DeviceSources &out);
 void free_sources(Context &ctx, DeviceSources &s);
 int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Executable &ex, void *shared_arena = nullptr);
-// vmm / need: a VMM arena not fully mapped yet and, per group, the prefix of
-// its mapping order the group needs (Program::vmm_need), mapped before the
-// group is enqueued; map_ms / first_ms: time spent mapping (all / before
-// the part's first group)
-int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks = nullptr, VmmArena *vmm = nullptr,
-           const std::vector<int> *need = nullptr, double *map_ms = nullptr, double *first_ms = nullptr);
+int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *hooks = nullptr);
 // waits for `stream`, downloads result tables: values as stored (double) and the exp2 scale
 int fetch_results(Context &ctx, Executable &ex, hipStream_t stream, std::vector<std::vector<double>> &vals,
                   std::vector<int64_t> &exp2);

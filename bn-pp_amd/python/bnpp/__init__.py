@@ -125,7 +125,7 @@ def _dbls(xs: Iterable[float]):
 
 
 TIMING_PHASES = ("plan_ms", "upload_ms", "program_ms", "launch_ms", "run_fetch_ms", "free_ms", "total_ms",
-                 "arena_reused", "arena_alloc_ms", "arena_map_ms", "arena_map_first_ms")
+                 "arena_reused", "arena_alloc_ms")
 
 
 def last_timing() -> Dict[str, float]:

@@ -71,14 +71,8 @@ static inline int bnpp_abi_matches(void) { return bnpp_version() == BNPP_VERSION
  *   out[6] total                                    out[7] 1 if the context's cached arena was reused
  *   out[8] of out[2]: the arena's hipMalloc (0 when reused) -- where a call
  *          waits for the driver to clear HBM that was freed shortly before
- *          (by any process: ~36 GB/s of backlog on MI355X);
- *          for an arena of 8 GiB or more: the address reservation only, its
- *          chunks being mapped as the launch loop reaches the first level
- *          that touches each --
- *   out[9] of out[3]: the arena chunks' mapping (the device runs the levels
- *          already enqueued meanwhile)    out[10] of out[9]: the part before
- *          the first level (exposed); both 0 when the arena was reused
- * Writes min(n, 11) values. */
+ *          (by any process: ~36 GB/s of backlog on MI355X)
+ * Writes min(n, 9) values. */
 int bnpp_last_timing(double *out, int n);
 
 /* ------------------------------------------------------------- device */

@@ -121,23 +121,10 @@ def test_tree_32x32_full_size_consistent_with_conditioned_partitions():
         assert len(marg) == 1024
         for t, p in marg.items():
             assert len(p) == 2 and min(p) >= 0.0 and abs(sum(p) - 1.0) < 1e-6, (t, p)
-        tm = bnpp.last_timing()
-        # the ~250-GB arena is a VMM range mapped chunk by chunk while the run
-        # goes (runtime.cpp VmmArena): the call reserved it and a helper mapped it
-        assert tm["arena_reused"] == 0.0 and tm["arena_map_ms"] > 0.0, tm
         lz = bnpp.partition(c, m, {}, "mf", bnpp.F32, order=col)[0]
         for t in (0, 527):
             lz0 = bnpp.partition(c, m, {t: 0}, "mf", bnpp.F32, order=col)[0]
             assert abs(10 ** (lz0 - lz) - marg[t][0]) < 1e-6, (t, 10 ** (lz0 - lz), marg[t])
-        # one hipMalloc'd arena instead (BNPP_NO_VMM=1): bit-identical marginals
-        c.trim()
-        os.environ["BNPP_NO_VMM"] = "1"
-        try:
-            marg1, _ = bnpp.marginals_tree(c, m, {}, "mf", bnpp.F32, order=col)
-            assert bnpp.last_timing()["arena_map_ms"] == 0.0
-        finally:
-            del os.environ["BNPP_NO_VMM"]
-        assert marg1 == marg
     finally:
         c.close()
 
