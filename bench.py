@@ -38,7 +38,8 @@ per-target and bucket-tree MAR (first call on a fresh model, as the
 reference's one-shot uptime; relaunch beside it), with the largest difference
 between them.  "fp64_bucket": the same k=4, w=14 bucket in the reference's
 precision (bit-exact path; 17.2 GB per launch), with its own roofline
-fraction.
+fraction.  "mar_f64": the 32x32 MAR in the reference's precision (fp64 split
+runs, 32-GiB messages), cold and warm, checked at 1e-11.
 
 N GPUs: `python bench.py --gpus N` outside a launcher starts the N ranks
 itself (python -m torch.distributed.run as a child process, before any GPU
@@ -348,6 +349,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-mar", action="store_true")
+    ap.add_argument("--no-mar-f64", action="store_true", help="skip the fp64 32x32 MAR (~25 s)")
     ap.add_argument("--no-fp64", action="store_true")
     ap.add_argument("--mar-rows", type=int, default=32)
     ap.add_argument("--mar-cols", type=int, default=32)
@@ -497,6 +499,16 @@ def main():
         reference_bound(mar, cpu["value"] if cpu else 7.2e6)   # r01 cpu_baseline when not run here
         if rank == 0:
             mar["secondary"] = secondary_mar(ctx, "ising10x10.uai", world == 1 and not args.no_cpu)
+    # the same 32x32 MAR in the reference's precision (fp64, factor.hh:46):
+    # split runs of 7 buckets, 32-GiB messages, 3 checkpoint slots in the arena
+    mar_f64 = None
+    if not args.no_mar and not args.no_mar_f64:
+        ctx.trim()                                         # the fp32 arena goes; the fp64 one takes its place
+        d = dist if world > 1 else None
+        mar_f64 = mar_wallclock(ctx, rank, world, d, dev, args.mar_rows, args.mar_cols, "f64", True)
+        mar_f64.pop("_model")
+        reference_bound(mar_f64, cpu["value"] if cpu else 7.2e6)
+        ctx.trim()
 
     # The sliced MAR (bnpp.dist.sliced_tree_marginals: every message split over
     # the ranks, one all-to-all per re-sliced message -- the north star's
@@ -530,6 +542,7 @@ def main():
                          "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "mar": mar,
+            "mar_f64": mar_f64,
             "fp64_bucket": fp64,
             "checksum_ok": ok,
             "spot_check_exact": spot_ok,
@@ -557,8 +570,9 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if mar and "check" in mar and not mar["check"]["ok"]:
-        ok = False
+    for rec in (mar, mar_f64):
+        if rec and "check" in rec and not rec["check"]["ok"]:
+            ok = False
     if fp64 is not None and not fp64["spot_check_exact"]:
         ok = False
     if not ok:

@@ -47,6 +47,7 @@
 #error "chainsplit.cuh: split chain runs need gfx950 (160 KiB LDS per workgroup)"
 #endif
 
+#include <algorithm>
 #include <mutex>
 
 namespace bnpp {
@@ -738,7 +739,10 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
         if (ds.attr[dev] != hipSuccess) return ds.attr[dev];
         cus = ds.cus[dev];
     }
-    const int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
+    // workgroups per CU: the wave target, capped by what fits the CU's LDS
+    // (an fp64 run of 7 buckets holds 130.5 KiB: one workgroup, 8 waves)
+    int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
+    per_cu = std::max(1, std::min<int>(per_cu, (int)((size_t)kSplitLdsBytes / shm)));
     const int64_t grid = a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
     if (a.n_desc == 1)
         hipLaunchKernelGGL((chain_split_kernel<T, F, FORM, DEP, DENSE, MODE1>), dim3((unsigned)grid),
