@@ -500,10 +500,12 @@ def main():
         if rank == 0:
             mar["secondary"] = secondary_mar(ctx, "ising10x10.uai", world == 1 and not args.no_cpu)
     # the same 32x32 MAR in the reference's precision (fp64, factor.hh:46):
-    # split runs of 7 buckets, 32-GiB messages, 3 checkpoint slots in the arena
+    # split runs of 7 buckets, 32-GiB messages, 3 checkpoint slots -- in the
+    # fp32 MAR's cached arena (the same size), as a serving process would run
+    # it: freeing that arena first made the fp64 call wait ~6 s for the
+    # driver to clear the 240 GB again
     mar_f64 = None
     if not args.no_mar and not args.no_mar_f64:
-        ctx.trim()                                         # the fp32 arena goes; the fp64 one takes its place
         d = dist if world > 1 else None
         mar_f64 = mar_wallclock(ctx, rank, world, d, dev, args.mar_rows, args.mar_cols, "f64", True)
         mar_f64.pop("_model")
