@@ -348,8 +348,37 @@ __device__ __forceinline__ void store_tiles(T *out, int64_t wave_tid0, int64_t n
     const int lane = threadIdx.x & 63;
     const int64_t tid = wave_tid0 + lane;
     constexpr int row_bytes = TS * (int)sizeof(T);
-    if constexpr (row_bytes <= 16 || BNPP_DIRECT_STORE != 0) {
+    if constexpr (row_bytes <= 8 || row_bytes == 16 || BNPP_DIRECT_STORE != 0) {
         if (tid < n_tiles) store_n<T, TS, kNtStore, true>(out + tid * TS, acc);
+    } else if constexpr (row_bytes % 16 != 0) {
+        // rows that are no whole number of 16-B chunks (a whole fastest dim
+        // of card 3, 5, 6 or 7 per thread): the wave's tiles are one run of
+        // 64 * TS consecutive entries, staged unpadded and stored as 16-B
+        // chunks (the run starts 16-B aligned: 64 * TS entries per wave)
+        constexpr int EPC = 16 / (int)sizeof(T);
+        constexpr int chunks = 64 * row_bytes / 16;
+        image_sync();
+        store_n<T, TS>(reinterpret_cast<T *>(lds + lane * row_bytes), acc);
+        image_sync();
+        const int64_t left = (n_tiles - wave_tid0) * TS;       // entries of this wave's tiles that exist
+        const int64_t valid = left < 64 * TS ? left : 64 * TS;
+        T *wout = out + wave_tid0 * TS;
+#pragma unroll
+        for (int it = 0; it < (chunks + 63) / 64; ++it) {
+            const int q = it * 64 + lane;
+            if (q < chunks) {
+                const int64_t e0 = (int64_t)q * EPC;
+                T x[EPC];
+                load_n<T, EPC>(reinterpret_cast<const T *>(lds + q * 16), x);
+                if (e0 + EPC <= valid) {
+                    store_n<T, EPC, kNtStore, true>(wout + e0, x);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e)
+                        if (e0 + e < valid) store_n<T, 1, kNtStore, true>(wout + e0 + e, x + e);
+                }
+            }
+        }
     } else {
         constexpr int rowp = row_bytes + kLdsRowPad;
         constexpr int cpr = row_bytes / 16;                   // 16-B chunks per row
@@ -934,10 +963,12 @@ static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_
 #define BNPP_CASE_SSINGLE(T, V1, V2, BC) \
     case 4096 + BC * 256 + V1 * 16 + V2: return go_stream_single<T, V1, V2, BC>(a, max_grid, stream);
 
+// (3, 1) (5, 1) (6, 1) (7, 1): a whole fastest dim of that card per thread
+#define BNPP_TILES_ODD(X, T, NIN) X(T, NIN, 3, 1) X(T, NIN, 5, 1) X(T, NIN, 6, 1) X(T, NIN, 7, 1)
 #define BNPP_TILES_F32(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
-    X(T, NIN, 4, 2) X(T, NIN, 4, 4) X(T, NIN, 2, 8)
+    X(T, NIN, 4, 2) X(T, NIN, 4, 4) X(T, NIN, 2, 8) BNPP_TILES_ODD(X, T, NIN)
 #define BNPP_TILES_F64(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
-    X(T, NIN, 4, 2)
+    X(T, NIN, 4, 2) BNPP_TILES_ODD(X, T, NIN)
 #define BNPP_ALL(X, TILES, T) TILES(X, T, 1) TILES(X, T, 2) TILES(X, T, 4) TILES(X, T, 8)
 
 #define BNPP_CASE_LEVEL(T, NIN, V1, V2) \

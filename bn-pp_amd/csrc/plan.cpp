@@ -842,6 +842,23 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
             }
         }
     }
+    // generic kernel, a fastest dim of card 3, 5, 6 or 7 (Munin1's card-7
+    // variables): 1x1 tiles paid a mixed-radix decode over every dim and one
+    // load per input per output; whole-dim tiles decode once per card0
+    // outputs and load stride-1 inputs as runs (scalar for odd cards, so no
+    // alignment; card 6 as pairs)
+    if (d.big < 0 && v1 == 1 && !merged.empty() && !b.simple) {
+        const uint64_t c0 = merged[0].card;
+        if ((c0 == 3 || c0 == 5 || c0 == 7 || (c0 == 6 && aligned(0, 2))) && (int)c0 <= max_tile) {
+            v1 = (int)c0;
+            v2 = 1;
+            d.v1 = v1;
+            d.v2 = 1;
+            d.n_tiles = out_size / v1;
+            divisor(1, d.tdiv0);
+            divisor(merged.size() < 2 ? 1 : merged[1].card, d.tdiv1);
+        }
+    }
     if (b.divide) {
         if (n != 2 || b.elim_var >= 0) {
             if (msg) *msg = "divide takes two inputs and sums nothing";
