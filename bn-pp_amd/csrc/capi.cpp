@@ -244,6 +244,23 @@ SlotMemo &slot_memo() {
     static SlotMemo m;
     return m;
 }
+// the plan-changing switches (kPlanKnobs); a tuning build (BNPP_TUNING_KNOBS)
+// keys on the whole BNPP_* environment, its knobs included
+template <typename Mix>
+void mix_plan_knobs(Mix &&mix) {
+#ifdef BNPP_TUNING_KNOBS
+    for (char **e = environ; e && *e; ++e)
+        if (std::strncmp(*e, "BNPP_", 5) == 0)
+            for (const char *c = *e; *c; ++c) mix((unsigned char)*c);
+#else
+    for (const char *k : kPlanKnobs) {
+        const char *v = std::getenv(k);
+        mix(0x9e37u);
+        for (const char *c = v ? v : ""; *c; ++c) mix((unsigned char)*c);
+    }
+#endif
+}
+
 uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<int>> &scopes, const std::vector<int> &ord,
                   const std::vector<int> &targets, int eb, int chain_eb, int part, int n_parts, int n_slices) {
     uint64_t h = 1469598103934665603ull;
@@ -262,13 +279,7 @@ uint64_t slot_key(const std::vector<int> &cards, const std::vector<std::vector<i
     mix((uint64_t)part);
     mix((uint64_t)n_parts);
     mix((uint64_t)n_slices);              // the slice rank does not change the arena need
-    // the planner's tuning knobs change the plan and its arena need
-    for (const char *k : {"BNPP_NO_SPLIT", "BNPP_NO_DENSE", "BNPP_NO_SIMPLE_LEVELS", "BNPP_SIMPLE_MAX", "BNPP_SPLIT_MIN_F", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_NO_REDUCE_MANY",
-                          "BNPP_CHAIN_RUN_MAX", "BNPP_NO_CHAIN_FWDV", "BNPP_NO_STREAM", "BNPP_NO_SLAB", "BNPP_MAX_TILE", "BNPP_SLICE_MIN_WIN"}) {
-        const char *v = std::getenv(k);
-        mix(0x9e37u);
-        for (const char *c = v ? v : ""; *c; ++c) mix((unsigned char)*c);
-    }
+    mix_plan_knobs(mix);                  // switches that change the plan and its arena need
     return h;
 }
 
@@ -345,7 +356,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             VEPlan best;
             // sliced runs: the two-front schedule (two concurrent lanes, no
             // recomputation) when its arena fits, else checkpointing on one lane
-            if (n_slices > 1 && !(std::getenv("BNPP_SLICE_LANES") && *std::getenv("BNPP_SLICE_LANES") == '0')) {
+            if (n_slices > 1 && !(tuning_knob("BNPP_SLICE_LANES") && *tuning_knob("BNPP_SLICE_LANES") == '0')) {
                 VEPlan cp;
                 if (plan_bucket_tree_chain(d.cards, views, ord, targets, 1, part, n_parts, cp, &msg, chain_eb, n_slices,
                                            slice_rank, true, eb)) {
@@ -746,9 +757,7 @@ uint64_t call_key(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, c
     mix((uint64_t)part);
     mix((uint64_t)n_parts);
     mix((uint64_t)(budget >> 30));                       // the plan depends on the budget (GiB)
-    for (char **e = environ; e && *e; ++e)               // planner / kernel knobs
-        if (std::strncmp(*e, "BNPP_", 5) == 0)
-            for (const char *c = *e; *c; ++c) mix((unsigned char)*c);
+    mix_plan_knobs(mix);
     return h ? h : 1;
 }
 
@@ -930,7 +939,7 @@ int bnpp_ctx_create(int device, bnpp_ctx **out) {
     std::unique_ptr<bnpp_ctx> ctx(new bnpp_ctx);
     ctx->c.device = device;
     int per_cu = 3;          // measured: 3 workgroups per CU beat 4 and 8 on the bench bucket and the 32x32 sweep
-    if (const char *g = std::getenv("BNPP_GRID_PER_CU")) per_cu = std::max(0, std::min(64, std::atoi(g)));
+    if (const char *g = tuning_knob("BNPP_GRID_PER_CU")) per_cu = std::max(0, std::min(64, std::atoi(g)));
     // 0: flat grid, one virtual block per workgroup (no grid-stride)
     ctx->c.max_grid = per_cu == 0 ? INT32_MAX : prop.multiProcessorCount * per_cu;
     if ((e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking)) != hipSuccess)

@@ -572,7 +572,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
     // inputs), then v2 entries of the next dim when v1 covers the whole fastest
     // dim (the tile is then v1*v2 contiguous output entries)
     int max_tile = max_vec == 2 ? 8 : 16;
-    if (const char *e = std::getenv("BNPP_MAX_TILE")) max_tile = std::max(1, std::min(max_tile, std::atoi(e)));
+    if (const char *e = tuning_knob("BNPP_MAX_TILE")) max_tile = std::max(1, std::min(max_tile, std::atoi(e)));
     if (b.simple) max_tile = 1;
     auto aligned = [&](int dim, int v) {
         for (int i = 0; i < n; ++i) {
@@ -636,7 +636,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
             else small_total += sp;
         }
         const int eb = max_vec == 2 ? 8 : 4;
-        const char *off = std::getenv("BNPP_NO_STREAM");
+        const char *off = tuning_knob("BNPP_NO_STREAM");
         if (!b.simple && !b.divide && n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 &&
             !(off && *off == '1')) {
             int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
@@ -663,7 +663,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 // [2 y][2^30 slab][2] k=2 ones ran 3.8 TB/s as one-pass slab tiles against
                 // 4.2 for the stream kernel, 4.5 with two passes (profiles/r04_slab_outer_ab.txt,
                 // r04_slab_passes_ab.txt)
-                const char *oc = std::getenv("BNPP_SLAB_OUTER_MAXC0");      // A/B knob
+                const char *oc = tuning_knob("BNPP_SLAB_OUTER_MAXC0");      // A/B knob
                 const int64_t max_c0 = oc ? std::atoll(oc) : 2;
                 if (slab_outer_n > 1 && (!slab_outer || (no && *no == '1') || slab_outer_n > kSlabMaxOuter ||
                                          (slab_dim == 1 && (int64_t)merged[0].card > max_c0)))
@@ -677,7 +677,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     int vn = eb == 4 ? (slab_c0 == 1 ? 4 : slab_c0 == 2 ? 2 : 1) : (slab_c0 == 1 ? 2 : 1);
                     // A/B knob: slow-dim entries per tile (instantiated: f32 c0=1 {1,4}, 2 {1,2},
                     // 4 {1,2}; f64 c0=1 {1,2}, 2 {1,2}, 4 {1}; slab.cuh)
-                    if (const char *sv = std::getenv("BNPP_SLAB_V")) {
+                    if (const char *sv = tuning_knob("BNPP_SLAB_V")) {
                         const int want = std::atoi(sv);
                         const bool inst = want == 1 || (want == 2 && slab_c0 != 1 && (eb == 4 || slab_c0 == 2)) ||
                                           (want == 2 && eb == 8 && slab_c0 == 1) || (want == 4 && eb == 4 && slab_c0 == 1);
@@ -689,7 +689,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     if (slab_outer_n > 1) {
                         // every combination's tiles fill whole virtual blocks
                         auto fits = [&](int v) {
-                            const char *sl = std::getenv("BNPP_SLAB_LANES");
+                            const char *sl = tuning_knob("BNPP_SLAB_LANES");
                             const int lanes = slab_c0 * v * eb == 32 && !(sl && *sl == '1') ? 2 : 1;
                             return ((int64_t)sd->card / v) % (kBlock / lanes) == 0;
                         };
@@ -708,7 +708,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 d.big = big;
                 d.bcls = kBigSlab;
                 // 32-B rows (f64 c0 * v = 4, f32 8): two lanes per tile, 16 B each
-                const char *sl = std::getenv("BNPP_SLAB_LANES");     // A/B knob: 1 = one lane per tile
+                const char *sl = tuning_knob("BNPP_SLAB_LANES");     // A/B knob: 1 = one lane per tile
                 d.lanes = v1 * v2 * eb == 32 && !(sl && *sl == '1') ? 2 : 1;
                 for (int i = 0; i < n; ++i) {
                     d.in_span[i] = (int32_t)std::min<int64_t>(span[i], INT32_MAX);
@@ -719,7 +719,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 // issued first (instantiated: f32 (C0, V) = (1, 4), (2, 2); f64 (1, 2); H = 1)
                 d.slab_r = 1;
                 {
-                    const char *sr = std::getenv("BNPP_SLAB_R");          // A/B knob: 1 = one pass
+                    const char *sr = tuning_knob("BNPP_SLAB_R");          // A/B knob: 1 = one pass
                     const bool inst = d.lanes == 1 && ((eb == 4 && ((v1 == 1 && v2 == 4) || (v1 == 2 && v2 == 2))) ||
                                                        (eb == 8 && v1 == 1 && v2 == 2));
                     if (slab_outer && !(sr && std::atoi(sr) == 1) && inst &&
@@ -750,7 +750,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
             // optional narrow tile: when the big input is constant along the
             // fastest output dim and v1 entries already fill a 16-B store, drop
             // v2 (one scalar big load per summed value, stores coalesced as is)
-            const char *nw = std::getenv("BNPP_NARROW");
+            const char *nw = tuning_knob("BNPP_NARROW");
             if (nw && *nw == '1' && v2 > 1 && s0 == 0 && v1 * eb >= 16) {
                 v2 = 1;
                 d.v2 = 1;
@@ -766,7 +766,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 for (size_t j = 1; inter && j < merged.size(); ++j)
                     if (merged[j].s[big] % vw) inter = false;
                 // wider tiles keep more bytes in flight per thread: 8 entries of dim 0
-                const char *iv = std::getenv("BNPP_INTER_V1");
+                const char *iv = tuning_knob("BNPP_INTER_V1");
                 const int want_v1 = iv ? std::atoi(iv) : 8;
                 int nv1 = v1;
                 if (want_v1 == 8 && merged[0].card % 8 == 0 && (int64_t)(8 * k) % vw == 0) nv1 = 8;
@@ -780,7 +780,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                         bdim = (int)j;
                         break;
                     }
-                const char *nb = std::getenv("BNPP_NO_BCAST_ROWS");
+                const char *nb = tuning_knob("BNPP_NO_BCAST_ROWS");
                 if (nb && *nb == '1') bdim = -1;
                 if (inter && bdim >= 1) {
                     const int cb = (int)merged[bdim].card;
@@ -1568,7 +1568,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         std::vector<int> win(m, -1);
         std::vector<std::vector<int>> Sw;
         if (sbits > 0) {
-            const char *mw = std::getenv("BNPP_SLICE_MIN_WIN");
+            const char *mw = tuning_knob("BNPP_SLICE_MIN_WIN");
             const int min_win = mw ? std::max(1, std::atoi(mw)) : 8;
             auto top_b = [&](int j, std::vector<int> &S) {
                 const std::vector<int> &sep = lam_vars[path[j]];
@@ -1926,7 +1926,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         std::vector<double> Wc(m + 1, 0.0);                    // Wc[i + 1] = entries of lam_0..lam_i
         for (int i = 0; i < m; ++i) Wc[i + 1] = Wc[i] + (double)table_size(lam_vars[path[i]], cards);
         auto adv_cost = [&](int from, int to) { return Wc[to + 1] - Wc[from + 1]; };
-        const bool use_dp = !lanes && nD > 0 && nD <= 256 && !std::getenv("BNPP_BINOMIAL_REVOLVE");
+        const bool use_dp = !lanes && nD > 0 && nD <= 256 && !tuning_knob("BNPP_BINOMIAL_REVOLVE");
         const int S = use_dp ? std::min(slots, nD) : 0;
         std::vector<double> cost;
         std::vector<int16_t> arg;
@@ -2401,7 +2401,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     // and is the fallback; it is a serial best-fit walk over every table
     // (136 ms for the 147,456 buckets of the 12x32 per-target MAR).
     bool placed = false;
-    const char *sa = std::getenv("BNPP_SHARED_ARENA");
+    const char *sa = tuning_knob("BNPP_SHARED_ARENA");
     if (plans.size() > 1 && !(sa && *sa == '1')) {
         std::vector<int64_t> tops(plans.size(), 0);
         std::vector<char> sat(plans.size(), 0);
@@ -2488,10 +2488,10 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     // ~9 tile / input-count variants per level, 1018 launches at 12x32) share
     // one generic 1x1 launch per level: launches, not bytes, bound them
     int64_t simple_max = 4096;                         // output entries (BNPP_SIMPLE_MAX: tuning)
-    if (const char *e = std::getenv("BNPP_SIMPLE_MAX")) simple_max = std::atoll(e);
+    if (const char *e = tuning_knob("BNPP_SIMPLE_MAX")) simple_max = std::atoll(e);
     std::vector<int> lvl_n(n_levels + 2, 0);
     for (const Item &it : items) ++lvl_n[it.level];
-    const char *ns = std::getenv("BNPP_NO_SIMPLE_LEVELS");
+    const char *ns = tuning_knob("BNPP_NO_SIMPLE_LEVELS");
     const bool simplify = !(ns && *ns == '1');
     parallel_for((int64_t)items.size(), [&](int64_t idx) {
         Item &it = items[idx];

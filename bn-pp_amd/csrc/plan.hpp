@@ -2,6 +2,7 @@
 #pragma once
 #include <cstdint>
 #include <climits>
+#include <cstdlib>
 #include <functional>
 #include <string>
 #include <memory>
@@ -11,6 +12,24 @@
 #include "bnpp_device.h"
 
 namespace bnpp {
+
+// Environment switches.  The product reads only the switches the tests use to
+// compare kernel forms and plan shapes bit for bit (BNPP_NO_CHAIN, _NO_SPLIT,
+// _NO_DENSE, _NO_SLAB, _NO_BEL_FUSE, _TREE_SLOTS, _KEEP_LOG2, ...), the memory
+// budget and diagnostics.  Tuning knobs -- launch shapes and layouts measured
+// once and settled (tools/) -- are read only by a build with
+// -DBNPP_TUNING_KNOBS (tools/build_variant.sh); elsewhere they read as unset.
+#ifdef BNPP_TUNING_KNOBS
+inline const char *tuning_knob(const char *name) { return std::getenv(name); }
+#else
+inline const char *tuning_knob(const char *) { return nullptr; }
+#endif
+// the switches that change a plan (the job cache and the slot memo key on them)
+constexpr const char *kPlanKnobs[] = {"BNPP_NO_CHAIN", "BNPP_NO_SPLIT", "BNPP_NO_DENSE", "BNPP_NO_SLAB",
+                                      "BNPP_NO_SLAB_OUTER", "BNPP_NO_BEL_FUSE", "BNPP_NO_CHAIN_FWDV",
+                                      "BNPP_NO_FREE_REDUCE", "BNPP_NO_REDUCE_MANY", "BNPP_NO_DEDUP",
+                                      "BNPP_TREE_SLOTS", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_SPLIT_MIN_F",
+                                      "BNPP_CHAIN_RUN_MAX", "BNPP_MEM_BUDGET_GB"};
 
 // Run body(i) for i in [0, n) on up to `threads` host threads (0: hardware
 // concurrency, capped at 16 — the per-GPU CPU share of the target machines).
