@@ -168,12 +168,17 @@ __device__ __forceinline__ void divmod_dim(uint64_t n, int64_t w0, int64_t w1, u
     }
 }
 
-struct LoadedBucket {
-    int64_t base[kMaxIn];
-    int64_t es[kMaxIn];
-    int64_t s0[kMaxIn];      // stride on the fastest output dim
-    int64_t s1[kMaxIn];      // stride on the second output dim
-    const void *ptr[kMaxIn];
+// NMAX: the input slots a kernel reads (the generic kernels' NIN class): the
+// per-input fields are uniform and belong in scalar registers, and sized for
+// eight inputs they overflowed them into vector registers (a 4-input 7x1
+// fp64 tile: 207 VGPRs)
+template <int NMAX>
+struct LoadedBucketT {
+    int64_t base[NMAX];
+    int64_t es[NMAX];
+    int64_t s0[NMAX];        // stride on the fastest output dim
+    int64_t s1[NMAX];        // stride on the second output dim
+    const void *ptr[NMAX];
     void *out;
     const int64_t *dims;     // dims pool rows, fastest first
     int64_t n_tiles;
@@ -181,6 +186,7 @@ struct LoadedBucket {
     int64_t t0h, t0m, t1h, t1m;
     int n_in, n_dims, k, v1, v2, flags, neg_e;
 };
+using LoadedBucket = LoadedBucketT<kMaxIn>;
 
 // One input's V1 x V2 tile (strides s0 / s1 along output dims 0 / 1), expanded.
 template <typename T, int V1, int V2>
@@ -226,7 +232,7 @@ __device__ __forceinline__ void load_tile(const T *src, int64_t s0, int64_t s1, 
 // Evaluate one V1 x V2 output tile: decode its mixed-radix position once, then
 // run the reference's product chain and sum in the reference's order.
 template <typename T, int NIN, int V1, int V2>
-__device__ __forceinline__ T compute_tile(const LoadedBucket &b, int64_t tid, T (&acc)[V1 * V2]) {
+__device__ __forceinline__ T compute_tile(const LoadedBucketT<NIN> &b, int64_t tid, T (&acc)[V1 * V2]) {
     constexpr int TS = V1 * V2;
     int64_t pos[NIN];
 #pragma unroll
@@ -401,14 +407,15 @@ __device__ __forceinline__ void store_tiles(T *out, int64_t wave_tid0, int64_t n
 }
 
 // fill the per-bucket register state from a descriptor + table pointers
-__device__ __forceinline__ void load_common(LoadedBucket &b, const BucketDesc &d, const int64_t *dims) {
+template <int NMAX>
+__device__ __forceinline__ void load_common(LoadedBucketT<NMAX> &b, const BucketDesc &d, const int64_t *dims) {
     b.n_in = d.n_in; b.n_dims = d.n_dims; b.k = d.k; b.v1 = d.v1; b.v2 = d.v2;
     b.n_tiles = d.n_tiles;
     b.dims = dims;
     b.t0h = d.tdiv0[0]; b.t0m = d.tdiv0[1]; b.t1h = d.tdiv1[0]; b.t1m = d.tdiv1[1];
     b.card0 = d.n_dims > 0 ? (int64_t)((uint64_t)dims[0] & 0xffffffffu) : 1;
     b.card1 = d.n_dims > 1 ? (int64_t)((uint64_t)dims[2 + d.n_in] & 0xffffffffu) : 1;
-    for (int i = 0; i < kMaxIn; ++i) {
+    for (int i = 0; i < NMAX; ++i) {
         bool on = i < d.n_in;
         b.base[i] = on ? d.in_base[i] : 0;
         b.es[i] = on ? d.elim_stride[i] : 0;
@@ -464,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
                                                               TableMeta *__restrict__ meta, int64_t total_vblocks) {
     __shared__ T red[kBlock / 64];
     __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * kLdsWaveBytes];
-    LoadedBucket b;
+    LoadedBucketT<NIN> b;
     int cur = -1;
     int64_t cur_begin = 0;
     T lmax = T(0);
@@ -480,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
             b.flags = d.flags;
             b.out = meta[d.out_table].ptr;
             int64_t e_sum = 0, x_sum = 0;
-            for (int i = 0; i < kMaxIn; ++i) {
+            for (int i = 0; i < NIN; ++i) {
                 if (i < d.n_in) {
                     const TableMeta &mi = meta[d.in_table[i]];
                     b.ptr[i] = mi.ptr;
@@ -525,12 +532,12 @@ __global__ __launch_bounds__(kBlock) void bucket_single_kernel(const SingleArgs 
     const SingleArgs &a = args;
 #endif
     const BucketDesc &d = a.d;
-    LoadedBucket b;
+    LoadedBucketT<NIN> b;
     load_common(b, d, a.pool);
     b.flags = d.flags & kDivide;
     b.neg_e = 0;
     b.out = a.meta[d.n_in].ptr;
-    for (int i = 0; i < kMaxIn; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : nullptr;
+    for (int i = 0; i < NIN; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : nullptr;
     __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * kLdsWaveBytes];
     for (int64_t tid0 = (int64_t)blockIdx.x * kBlock; tid0 < b.n_tiles; tid0 += (int64_t)gridDim.x * kBlock) {
         const int64_t tid = tid0 + threadIdx.x;
