@@ -252,8 +252,10 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     static_assert(W * EB <= kRedBytes, "reduction scratch");
     static_assert(EB == 4 || F <= 7, "fp64 split runs: F <= 7 (LDS)");
     // fp64: the row image and exchange table leave room for one workgroup
-    // (8 waves at F = 7) per CU, so two tiles' loads are kept in flight
-    // instead of one (2 waves per SIMD: the registers are there)
+    // (8 waves at F = 7) per CU, so forward runs keep two tiles' loads in
+    // flight instead of one (2 waves per SIMD: the registers are there):
+    // 17.08 -> 16.34 ms per 2^32-entry message; the backward runs got slower
+    // that way (17.12 -> 17.57 ms) and keep one (profiles/r05_f64_ahead2.txt)
     constexpr bool AHEAD2 = EB == 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
@@ -631,40 +633,6 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         // (2) the lam loads are unconditional in a loop of their own -- issued
         // under a branch, the merge at the branch's join took the path without
         // them and drained them at the top of the tile as well
-        if constexpr (AHEAD2) {
-            // fp64: two tiles' rows in flight, in two register sets used in
-            // turn by a loop unrolled twice (no set is copied at the latch)
-            T rg2[16];
-            decode(vb, in_off, out_off, gb);
-            issue(in_off, rg);
-            decode(vb + gridDim.x < total_vblocks ? vb + gridDim.x : total_vblocks - 1, in_off, out_off, gb);
-            issue(in_off, rg2);
-            __builtin_amdgcn_s_waitcnt(0x0f70);            // vmcnt(0): the first two tiles' rows
-            auto run2 = [&](auto belc) {
-                constexpr bool BEL = decltype(belc)::value;
-                auto step = [&](T (&rx)[16]) {
-                    T t[16];
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) t[e] = rx[e];
-                    if constexpr (BEL) {
-                        decode(vb, in_off, out_off, gb);
-                        load_lam(tout);
-                    }
-                    const int64_t vb2 = vb + 2 * (int64_t)gridDim.x;
-                    decode(vb2 < total_vblocks ? vb2 : total_vblocks - 1, in_off, out_off, gb);
-                    issue(in_off, rx);
-                    decode(vb, in_off, out_off, gb);
-                    run_tile(std::integral_constant<int, BEL ? 1 : 0>{}, t, out_off, gb);
-                    vb += gridDim.x;
-                    return vb < total_vblocks;
-                };
-                while (step(rg) && step(rg2)) {
-                }
-            };
-            run2(std::integral_constant<bool, DENSE && MODE == 1>{});
-            flush();
-            return;
-        }
         decode(vb, in_off, out_off, gb);
         issue(in_off, rg);
         __builtin_amdgcn_s_waitcnt(0x0f70);                // vmcnt(0): the first tile's rows
