@@ -232,9 +232,6 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // without a belief to that many waves per SIMD (4: 128 VGPRs, the persistent
 // grid's 16 waves per CU, at the price of a few spilled registers; left
 // alone they take 128-164 VGPRs, 3 waves)
-#ifndef BNPP_F32_FWD_AHEAD2
-#define BNPP_F32_FWD_AHEAD2 1      // fp32 dense forward runs: two tiles ahead (variant builds: 0 = one)
-#endif
 #ifndef BNPP_F64_SPLIT_WAVES
 #define BNPP_F64_SPLIT_WAVES 1
 #endif
@@ -258,8 +255,9 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     // (8 waves at F = 7) per CU, so forward runs keep two tiles' loads in
     // flight instead of one (2 waves per SIMD: the registers are there):
     // 17.08 -> 16.34 ms per 2^32-entry message; the backward runs got slower
-    // that way (17.12 -> 17.57 ms) and keep one (profiles/r05_f64_ahead2.txt)
-    constexpr bool AHEAD2 = EB == 8 || (DENSE && BNPP_F32_FWD_AHEAD2 != 0);
+    // that way (17.12 -> 17.57 ms) and keep one, and so did fp32 forward runs
+    // at 16 waves per CU (5.99 -> 6.23 ms; profiles/r05_f64_ahead2.txt)
+    constexpr bool AHEAD2 = EB == 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     T *red = reinterpret_cast<T *>(dyn);
     T *xch = reinterpret_cast<T *>(dyn + kRedBytes);
