@@ -52,6 +52,10 @@ struct bnpp_ctx {
     bnpp_job *job_cached = nullptr;
     uint64_t job_key = 0;
 };
+// live contexts: bnpp_model_free releases what they cache for the model
+std::mutex g_ctxs_mu;
+std::vector<bnpp_ctx *> g_ctxs;
+
 struct bnpp_model {
     ModelData d;
     uint64_t uid = next_uid();
@@ -63,6 +67,7 @@ struct bnpp_model {
 struct bnpp_job {
     bnpp_ctx *ctx = nullptr;
     int kind = 0;
+    uint64_t model_uid = 0;            // the model it was planned for (bnpp_model_free evicts a cached job of it)
     std::shared_ptr<DeviceSources> src;
     Program pg;
     std::vector<int> targets;
@@ -673,6 +678,7 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     job.reset(new bnpp_job);
     job->ctx = ctx;
     job->kind = kind;
+    job->model_uid = m->uid;
     job->cards = d.cards;
     job->n_slices = n_slices;
     job->slice_rank = slice_rank;
@@ -944,6 +950,10 @@ int bnpp_ctx_create(int device, bnpp_ctx **out) {
     ctx->c.max_grid = per_cu == 0 ? INT32_MAX : prop.multiProcessorCount * per_cu;
     if ((e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking)) != hipSuccess)
         return set_err(BNPP_ERR_HIP, hipGetErrorString(e));
+    {
+        std::lock_guard<std::mutex> g(g_ctxs_mu);
+        g_ctxs.push_back(ctx.get());
+    }
     *out = ctx.release();
     return BNPP_OK;
     BNPP_GUARD_END
@@ -951,6 +961,10 @@ int bnpp_ctx_create(int device, bnpp_ctx **out) {
 
 int bnpp_ctx_destroy(bnpp_ctx *ctx) {
     if (!ctx) return BNPP_OK;
+    {
+        std::lock_guard<std::mutex> g(g_ctxs_mu);
+        g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), ctx), g_ctxs.end());
+    }
     (void)hipSetDevice(ctx->c.device);
     evict_cached_job(ctx);
     if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
@@ -1196,6 +1210,21 @@ int bnpp_model_from_arrays(int is_bayes, int n_vars, const int *cards, int n_fac
 }
 
 int bnpp_model_free(bnpp_model *m) {
+    if (!m) return BNPP_OK;
+    // every live context drops the model's uploaded sources and a cached
+    // one-shot job planned for it (a context in the middle of a call keeps
+    // its job until its next one-shot call replaces it)
+    std::lock_guard<std::mutex> g(g_ctxs_mu);
+    for (bnpp_ctx *ctx : g_ctxs) {
+        {
+            std::lock_guard<std::mutex> gs(ctx->src_mu);
+            ctx->srcs.erase(std::remove_if(ctx->srcs.begin(), ctx->srcs.end(),
+                                           [&](const bnpp_ctx::Src &e) { return e.uid == m->uid; }),
+                            ctx->srcs.end());
+        }
+        std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
+        if (lk.owns_lock() && ctx->job_cached && ctx->job_cached->model_uid == m->uid) evict_cached_job(ctx);
+    }
     delete m;
     return BNPP_OK;
 }

@@ -159,6 +159,10 @@ int bnpp_model_load_uai(const char *path, bnpp_model **out);
 /* the same data from arrays: scopes concatenated, values concatenated (row-major) */
 int bnpp_model_from_arrays(int is_bayes, int n_vars, const int *cards, int n_factors, const int *widths,
                            const int *scopes, const double *values, bnpp_model **out);
+/* Frees the model; every live context also drops what it caches for it (its
+ * uploaded sources and a cached one-shot job planned for it -- a context in the
+ * middle of a call keeps its job until its next one-shot call replaces it).
+ * The contexts' cached arena is not the model's and stays: bnpp_ctx_trim. */
 int bnpp_model_free(bnpp_model *m);
 int bnpp_model_info(const bnpp_model *m, int *is_bayes, int *n_vars, int *n_factors);
 int bnpp_model_cards(const bnpp_model *m, int *cards);

@@ -631,3 +631,21 @@ def test_job_cache_never_serves_invalid_evidence(ctx):
             with pytest.raises(bnpp.BnppError):
                 call(bad)
         call({})
+
+
+def test_model_free_releases_cached_job_and_sources(ctx):
+    """bnpp_model_free drops the contexts' cached sources and one-shot job of
+    the freed model (capi.cpp): later calls on other models are unaffected and
+    still equal the oracle."""
+    from bnpp import synth
+    import gc
+    d = synth.ising_grid(5, 5, seed=9)
+    m = bnpp.Model.from_dict(d)
+    z = bnpp.partition(ctx, m, {}, "mf", bnpp.F64)[1]
+    bnpp.marginals_tree(ctx, m, {}, "mf", bnpp.F64)
+    del m
+    gc.collect()
+    m2 = bnpp.Model.from_dict(d)
+    z2 = bnpp.partition(ctx, m2, {}, "mf", bnpp.F64)[1]
+    assert bnpp.last_timing()["plan_ms"] > 0.0             # a new model: planned afresh
+    assert z == z2 == refcpu.Model.from_dict(d).partition({}, "mf")[0]
