@@ -18,7 +18,8 @@ from collections import defaultdict
 def per_kernel(path, counter):
     out = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and "chain_split_kernel<8" in r["Kernel_Name"]:
+        if r["Counter_Name"] == counter and ("chain_split_kernel<8" in r["Kernel_Name"] or
+                                             "chain_split_kernel<float, 8" in r["Kernel_Name"]):
             out[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]) * 1024)
     return out
 
