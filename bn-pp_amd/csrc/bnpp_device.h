@@ -125,6 +125,10 @@ constexpr int kStreamLdsBudget = 32768;    // bytes of LDS for the small inputs
 // launch gets the register allocation of its own shape.
 __host__ __device__ inline int nin_class(int n_in) { return n_in <= 1 ? 1 : n_in <= 2 ? 2 : n_in <= 4 ? 4 : 8; }
 __host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return nin_class(n_in) * 64 + v1 * 8 + v2; }
+// + kGenericO32: the same kernel with 32-bit table offsets, for launches whose
+// every input is under 4 GiB (generic_o32)
+constexpr int kGenericO32 = 1024;
+__host__ __device__ inline bool generic_o32(int64_t max_in_bytes) { return max_in_bytes <= (int64_t)0xffffffff; }
 // stream kernels: 4096 + big-class * 256 + v1 * 16 + v2  (v1, v2 <= 8)
 __host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 256 + v1 * 16 + v2; }
 // slab kernels (slab.cuh): K summed values, C0 entries of output dim 0, V slow-dim entries per lane

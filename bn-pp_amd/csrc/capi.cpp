@@ -138,7 +138,15 @@ int run_single(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &c
         return set_err(BNPP_ERR_UNSUPPORTED, "too many non-mergeable output dims for a single-op call");
     std::copy(pool.begin(), pool.end(), a.pool);
     a.d.dim_off = 0;
-    for (size_t i = 0; i < in_ptrs.size(); ++i) a.meta[i].ptr = const_cast<void *>(in_ptrs[i]);
+    for (size_t i = 0; i < in_ptrs.size(); ++i) {
+        a.meta[i].ptr = const_cast<void *>(in_ptrs[i]);
+        // entries the view can reach (the launcher picks 32-bit offsets by it)
+        const View &v = b.in[i];
+        int64_t span = v.base + 1;
+        for (size_t j = 0; j < v.vars.size() && j < v.strides.size(); ++j)
+            span += sat_mul(cards[v.vars[j]] - 1, v.strides[j]);
+        a.meta[i].size = span;
+    }
     a.meta[in_ptrs.size()].ptr = out;
     if (a.d.big >= 0) {
         const int eb = dtype == BNPP_F32 ? 4 : 8;

@@ -188,79 +188,109 @@ struct LoadedBucketT {
 };
 using LoadedBucket = LoadedBucketT<kMaxIn>;
 
-// One input's V1 x V2 tile (strides s0 / s1 along output dims 0 / 1), expanded.
-template <typename T, int V1, int V2>
-__device__ __forceinline__ void load_tile(const T *src, int64_t s0, int64_t s1, T (&x)[V1 * V2]) {
-    constexpr int TS = V1 * V2;
+// Element `off` of a table.  O32: a 32-bit offset added to the table's
+// uniform base (global_load ... vOff, s[base] -- one address VGPR per load
+// instead of two, and no 64-bit address arithmetic); used when every input
+// of the launch is under 4 GiB.
+template <bool O32>
+using toff_t = typename std::conditional<O32, uint32_t, int64_t>::type;
+template <bool O32, typename T>
+__device__ __forceinline__ const T *tptr(const T *base, toff_t<O32> off) {
+    if constexpr (O32) return (const T *)((const char *)base + (uint32_t)(off * (uint32_t)sizeof(T)));
+    else return base + off;
+}
+
+// One input's V1 x V2 tile (strides s0 / s1 along output dims 0 / 1).  The
+// values stay where their loads put them -- a broadcast input fills x[0] (or
+// x[j2 * V1] per row, or one row x[0 .. V1)) -- and expand_tile spreads them
+// once every input's loads are in flight.  Expanding here (x[j] = y) would
+// make the copy wait for its load, and vmcnt counts in issue order: every
+// input's loads would finish before the next input's were issued.
+template <typename T, int V1, int V2, bool O32>
+__device__ __forceinline__ void load_tile(const T *base, toff_t<O32> off, int64_t s0_, int64_t s1_,
+                                          T (&x)[V1 * V2]) {
+    const toff_t<O32> s0 = (toff_t<O32>)s0_, s1 = (toff_t<O32>)s1_;
+    const bool row1 = V2 == 1 || s1 == 0;                 // the same along dim 1
     if (s0 == 0) {
-        if (V2 == 1 || s1 == 0) {                         // broadcast over the tile
-            T y = gload(src);
-#pragma unroll
-            for (int j = 0; j < TS; ++j) x[j] = y;
+        if (row1) {
+            x[0] = gload(tptr<O32>(base, off));
         } else {
-            T y[V2];
-            if (s1 == 1) load_n<T, V2, false, true>(src, y);
-            else {
 #pragma unroll
-                for (int j2 = 0; j2 < V2; ++j2) y[j2] = gload(src + (int64_t)j2 * s1);
-            }
-#pragma unroll
-            for (int j2 = 0; j2 < V2; ++j2)
-#pragma unroll
-                for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = y[j2];
+            for (int j2 = 0; j2 < V2; ++j2) x[j2 * V1] = gload(tptr<O32>(base, off + j2 * s1));
         }
     } else if (V1 > 1 && s0 == 1) {                       // contiguous along the fastest dim
-        if (V2 == 1 || s1 == 0) {
-            T y[V1];
-            load_n<T, V1, false, true>(src, y);
-#pragma unroll
-            for (int j2 = 0; j2 < V2; ++j2)
-#pragma unroll
-                for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = y[j1];
+        if (row1) {
+            load_n<T, V1, false, true>(tptr<O32>(base, off), x);
         } else {
 #pragma unroll
-            for (int j2 = 0; j2 < V2; ++j2) load_n<T, V1, false, true>(src + (int64_t)j2 * s1, x + j2 * V1);
+            for (int j2 = 0; j2 < V2; ++j2) load_n<T, V1, false, true>(tptr<O32>(base, off + j2 * s1), x + j2 * V1);
         }
     } else {                                              // general gather
 #pragma unroll
         for (int j2 = 0; j2 < V2; ++j2)
 #pragma unroll
-            for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = gload(src + (int64_t)j1 * s0 + (int64_t)j2 * s1);
+            for (int j1 = 0; j1 < V1; ++j1)
+                if (j2 == 0 || !row1) x[j2 * V1 + j1] = gload(tptr<O32>(base, off + j1 * s0 + j2 * s1));
+    }
+}
+
+// spread what load_tile left compact over the whole tile
+template <typename T, int V1, int V2>
+__device__ __forceinline__ void expand_tile(T (&x)[V1 * V2], int64_t s0, int64_t s1) {
+    const bool row1 = V2 == 1 || s1 == 0;
+    if (s0 == 0 && row1) {
+#pragma unroll
+        for (int j = 1; j < V1 * V2; ++j) x[j] = x[0];
+    } else if (s0 == 0) {
+#pragma unroll
+        for (int j2 = 0; j2 < V2; ++j2)
+#pragma unroll
+            for (int j1 = 1; j1 < V1; ++j1) x[j2 * V1 + j1] = x[j2 * V1];
+    } else if (row1) {
+#pragma unroll
+        for (int j2 = 1; j2 < V2; ++j2)
+#pragma unroll
+            for (int j1 = 0; j1 < V1; ++j1) x[j2 * V1 + j1] = x[j1];
     }
 }
 
 // Evaluate one V1 x V2 output tile: decode its mixed-radix position once, then
 // run the reference's product chain and sum in the reference's order.
-template <typename T, int NIN, int V1, int V2>
+template <typename T, int NIN, int V1, int V2, bool O32>
 __device__ __forceinline__ T compute_tile(const LoadedBucketT<NIN> &b, int64_t tid, T (&acc)[V1 * V2]) {
     constexpr int TS = V1 * V2;
-    int64_t pos[NIN];
+    using O = toff_t<O32>;
+    O pos[NIN];
 #pragma unroll
-    for (int i = 0; i < NIN; ++i) pos[i] = b.base[i];
+    for (int i = 0; i < NIN; ++i) pos[i] = (O)b.base[i];
     int64_t obase = 0;
     if (b.n_dims > 0) {
         uint64_t q, r;
         divmod_dim((uint64_t)tid, b.t0h, b.t0m, q, r);
         int64_t i0 = (int64_t)r * V1;
 #pragma unroll
-        for (int i = 0; i < NIN; ++i) pos[i] += i0 * b.s0[i];
+        for (int i = 0; i < NIN; ++i) pos[i] += (O)i0 * (O)b.s0[i];
         obase = i0;
         if (b.n_dims > 1) {
             uint64_t q1, r1;
             divmod_dim(q, b.t1h, b.t1m, q1, r1);
             int64_t i1 = (int64_t)r1 * V2;
 #pragma unroll
-            for (int i = 0; i < NIN; ++i) pos[i] += i1 * b.s1[i];
+            for (int i = 0; i < NIN; ++i) pos[i] += (O)i1 * (O)b.s1[i];
             obase = ((int64_t)q1 * b.card1 + i1) * b.card0 + i0;
             uint64_t rem = q1;
             const int row = 2 + b.n_in;                  // dims-pool row length
-            const int64_t *dp = b.dims + 2 * row;
+            // the pool is read-only while kernels run and its address is
+            // uniform: read it through the scalar cache (constant address
+            // space) instead of a vector load and a wait per dim
+            const __attribute__((address_space(4))) int64_t *dp =
+                (const __attribute__((address_space(4))) int64_t *)(b.dims + 2 * row);
             for (int j = 2; j < b.n_dims; ++j) {
                 uint64_t qq, rr;
                 divmod_dim(rem, dp[0], dp[1], qq, rr);
 #pragma unroll
                 for (int i = 0; i < NIN; ++i)
-                    if (i < b.n_in) pos[i] += (int64_t)rr * dp[2 + i];
+                    if (i < b.n_in) pos[i] += (O)rr * (O)dp[2 + i];
                 rem = qq;
                 dp += row;
             }
@@ -272,22 +302,29 @@ __device__ __forceinline__ T compute_tile(const LoadedBucketT<NIN> &b, int64_t t
     // Every input's loads for VB consecutive summed values are issued before
     // the first product uses one: loading and multiplying input by input
     // leaves one load in flight per thread, and a gather-heavy bucket (Munin1's
-    // largest: 3 inputs x 7 values per output, 1x1 tiles) then pays 21 memory
-    // round trips per output in series (1.78 ms for 39 M outputs).  The
-    // arithmetic that follows is unchanged: p = 1; p *= in_0; ...; acc += p
-    // per summed value in order (factor.cpp:131-143, 199-205).
+    // largest: 3 inputs x 7 values per output) then pays a memory round trip
+    // per input and summed value in series.  Unused input slots (i >= n_in)
+    // read entry 0 of input 0 (load_common), so the loads are issued without a
+    // branch per slot.  The arithmetic that follows is unchanged: p = 1;
+    // p *= in_0; ...; acc += p per summed value in order (factor.cpp:131-143,
+    // 199-205).
     constexpr int VB = TS * NIN >= 16 ? 1 : 16 / (TS * NIN);
     for (int v0 = 0; v0 < b.k; v0 += VB) {
         T x[VB][NIN][TS];
 #pragma unroll
         for (int vv = 0; vv < VB; ++vv) {
-            const int64_t v = v0 + vv;
+            const O v = (O)(v0 + vv);
 #pragma unroll
             for (int i = 0; i < NIN; ++i)
-                if (v < b.k && i < b.n_in)                 // uniform
-                    load_tile<T, V1, V2>(static_cast<const T *>(b.ptr[i]) + pos[i] + v * b.es[i], b.s0[i], b.s1[i],
-                                         x[vv][i]);
+                if (VB == 1 || v0 + vv < b.k)              // uniform
+                    load_tile<T, V1, V2, O32>(static_cast<const T *>(b.ptr[i]), pos[i] + v * (O)b.es[i], b.s0[i],
+                                              b.s1[i], x[vv][i]);
         }
+#pragma unroll
+        for (int vv = 0; vv < VB; ++vv)
+#pragma unroll
+            for (int i = 0; i < NIN; ++i)
+                if (v0 + vv < b.k && i < b.n_in) expand_tile<T, V1, V2>(x[vv][i], b.s0[i], b.s1[i]);
 #pragma unroll
         for (int vv = 0; vv < VB; ++vv) {
             if (v0 + vv < b.k) {                           // uniform
@@ -406,12 +443,22 @@ __device__ __forceinline__ void store_tiles(T *out, int64_t wave_tid0, int64_t n
     }
 }
 
+// uniform read-only data (descriptors, the dims pool, table pointers) read
+// through the scalar cache: the compiler cannot prove on its own that the
+// kernel's stores leave them alone, and reads them with vector loads into
+// vector registers
+template <typename T>
+using cst_t = const __attribute__((address_space(4))) T;
+template <typename T>
+__device__ __forceinline__ cst_t<T> *as_const(const T *p) { return (cst_t<T> *)p; }
+
 // fill the per-bucket register state from a descriptor + table pointers
-template <int NMAX>
-__device__ __forceinline__ void load_common(LoadedBucketT<NMAX> &b, const BucketDesc &d, const int64_t *dims) {
+template <int NMAX, typename D>
+__device__ __forceinline__ void load_common(LoadedBucketT<NMAX> &b, const D &d, const int64_t *dims_) {
+    cst_t<int64_t> *dims = as_const(dims_);
     b.n_in = d.n_in; b.n_dims = d.n_dims; b.k = d.k; b.v1 = d.v1; b.v2 = d.v2;
     b.n_tiles = d.n_tiles;
-    b.dims = dims;
+    b.dims = dims_;
     b.t0h = d.tdiv0[0]; b.t0m = d.tdiv0[1]; b.t1h = d.tdiv1[0]; b.t1m = d.tdiv1[1];
     b.card0 = d.n_dims > 0 ? (int64_t)((uint64_t)dims[0] & 0xffffffffu) : 1;
     b.card1 = d.n_dims > 1 ? (int64_t)((uint64_t)dims[2 + d.n_in] & 0xffffffffu) : 1;
@@ -465,7 +512,7 @@ __device__ __forceinline__ int find_bucket(const BucketDesc *descs, int n_desc, 
     return lo;
 }
 
-template <typename T, int NIN, int V1, int V2>
+template <typename T, int NIN, int V1, int V2, bool O32>
 __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                               const int64_t *__restrict__ pool,
                                                               TableMeta *__restrict__ meta, int64_t total_vblocks) {
@@ -481,7 +528,7 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
             if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
             cur = bi;
             lmax = T(0);
-            const BucketDesc &d = descs[bi];
+            cst_t<BucketDesc> &d = *as_const(descs + bi);
             cur_begin = d.vblk_begin;
             load_common(b, d, pool + d.dim_off);
             b.flags = d.flags;
@@ -489,7 +536,9 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
             int64_t e_sum = 0, x_sum = 0;
             for (int i = 0; i < NIN; ++i) {
                 if (i < d.n_in) {
-                    const TableMeta &mi = meta[d.in_table[i]];
+                    // the input tables' metadata is final (written by earlier
+                    // launches); only the output's changes in this one
+                    cst_t<TableMeta> &mi = *as_const(meta + d.in_table[i]);
                     b.ptr[i] = mi.ptr;
                     int e = FBits<T>::exponent(mi.maxbits);
                     if (d.flags & kScale) {
@@ -499,7 +548,7 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
                         x_sum += mi.exp2;
                     }
                 } else {
-                    b.ptr[i] = nullptr;
+                    b.ptr[i] = b.ptr[0];                   // unused slot: compute_tile reads entry 0
                 }
             }
             b.neg_e = (int)(-e_sum);
@@ -510,7 +559,7 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
         const int64_t tid = tid0 + threadIdx.x;
         T acc[V1 * V2];
         if (tid < b.n_tiles) {
-            T m = compute_tile<T, NIN, V1, V2>(b, tid, acc);
+            T m = compute_tile<T, NIN, V1, V2, O32>(b, tid, acc);
             lmax = m > lmax ? m : lmax;
         }
         store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
@@ -521,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
 
 // One bucket whose descriptor travels in the kernel-argument segment: used by
 // the single-op API (Factor::product / sum_out / conditioning), no rescaling.
-template <typename T, int NIN, int V1, int V2>
+template <typename T, int NIN, int V1, int V2, bool O32>
 __global__ __launch_bounds__(kBlock) void bucket_single_kernel(const SingleArgs args) {
     // read the argument block in place (constant address space, scalar loads)
     // instead of letting the compiler copy it to scratch
@@ -537,12 +586,12 @@ __global__ __launch_bounds__(kBlock) void bucket_single_kernel(const SingleArgs 
     b.flags = d.flags & kDivide;
     b.neg_e = 0;
     b.out = a.meta[d.n_in].ptr;
-    for (int i = 0; i < NIN; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : nullptr;
+    for (int i = 0; i < NIN; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : a.meta[0].ptr;
     __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * kLdsWaveBytes];
     for (int64_t tid0 = (int64_t)blockIdx.x * kBlock; tid0 < b.n_tiles; tid0 += (int64_t)gridDim.x * kBlock) {
         const int64_t tid = tid0 + threadIdx.x;
         T acc[V1 * V2];
-        if (tid < b.n_tiles) (void)compute_tile<T, NIN, V1, V2>(b, tid, acc);
+        if (tid < b.n_tiles) (void)compute_tile<T, NIN, V1, V2, O32>(b, tid, acc);
         store_tiles<T, V1 * V2>(static_cast<T *>(b.out), tid0 + (threadIdx.x & ~63), b.n_tiles, acc,
                                 lds + (threadIdx.x >> 6) * kLdsWaveBytes);
     }
@@ -922,19 +971,19 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_single_ke
 
 // ---------------------------------------------------------------- launchers
 
-template <typename T, int NIN, int V1, int V2>
+template <typename T, int NIN, int V1, int V2, bool O32>
 static hipError_t go_level(const LevelArgs &a, int max_grid, hipStream_t stream) {
     int64_t grid = a.vblocks < max_grid ? a.vblocks : max_grid;
-    hipLaunchKernelGGL((bucket_level_kernel<T, NIN, V1, V2>), dim3((unsigned)grid), dim3(kBlock), 0, stream, a.descs,
+    hipLaunchKernelGGL((bucket_level_kernel<T, NIN, V1, V2, O32>), dim3((unsigned)grid), dim3(kBlock), 0, stream, a.descs,
                        a.n_desc, a.pool, a.meta, a.vblocks);
     return hipGetLastError();
 }
 
-template <typename T, int NIN, int V1, int V2>
+template <typename T, int NIN, int V1, int V2, bool O32>
 static hipError_t go_single(const SingleArgs &a, int max_grid, hipStream_t stream) {
     int64_t blocks = (a.d.n_tiles + kBlock - 1) / kBlock;
     int64_t grid = blocks < max_grid ? blocks : max_grid;
-    hipLaunchKernelGGL((bucket_single_kernel<T, NIN, V1, V2>), dim3((unsigned)grid), dim3(kBlock), 0, stream, a);
+    hipLaunchKernelGGL((bucket_single_kernel<T, NIN, V1, V2, O32>), dim3((unsigned)grid), dim3(kBlock), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -979,9 +1028,11 @@ static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_
 #define BNPP_ALL(X, TILES, T) TILES(X, T, 1) TILES(X, T, 2) TILES(X, T, 4) TILES(X, T, 8)
 
 #define BNPP_CASE_LEVEL(T, NIN, V1, V2) \
-    case NIN * 64 + V1 * 8 + V2: return go_level<T, NIN, V1, V2>(a, max_grid, stream);
+    case NIN * 64 + V1 * 8 + V2: return go_level<T, NIN, V1, V2, false>(a, max_grid, stream); \
+    case kGenericO32 + NIN * 64 + V1 * 8 + V2: return go_level<T, NIN, V1, V2, true>(a, max_grid, stream);
 #define BNPP_CASE_SINGLE(T, NIN, V1, V2) \
-    case NIN * 64 + V1 * 8 + V2: return go_single<T, NIN, V1, V2>(a, max_grid, stream);
+    case NIN * 64 + V1 * 8 + V2: return go_single<T, NIN, V1, V2, false>(a, max_grid, stream); \
+    case kGenericO32 + NIN * 64 + V1 * 8 + V2: return go_single<T, NIN, V1, V2, true>(a, max_grid, stream);
 
 
 }  // namespace bnpp

@@ -65,7 +65,10 @@ hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStrea
         return is_f32 ? dispatch_stream_single_f32(key, a, max_grid, stream)
                       : dispatch_stream_single_f64(key, a, max_grid, stream);
     }
-    const int key = variant_key(a.d.n_in, a.d.v1, a.d.v2);
+    int64_t in_bytes = 0;
+    for (int i = 0; i < a.d.n_in && i < kMaxIn; ++i)
+        in_bytes = std::max<int64_t>(in_bytes, a.meta[i].size * (is_f32 ? 4 : 8));
+    const int key = variant_key(a.d.n_in, a.d.v1, a.d.v2) + (generic_o32(in_bytes) ? kGenericO32 : 0);
     return is_f32 ? dispatch_single_f32(key, a, max_grid, stream) : dispatch_single_f64(key, a, max_grid, stream);
 }
 

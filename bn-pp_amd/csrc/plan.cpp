@@ -2514,12 +2514,18 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         }
         const std::vector<int> &pc = plans[it.plan]->cards_ext.empty() ? cards : plans[it.plan]->cards_ext;
         it.ok = build_desc(b, pc, max_vec, it.d, it.pool, &it.msg);
+        auto max_in_bytes = [&](const BucketSpec &bs) {
+            int64_t m = 0;
+            for (const View &v : bs.in) m = std::max(m, sat_mul(s.table_size[v.table], elem_bytes));
+            return m;
+        };
         it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf) +
                                   ((it.d.flags & kChainBel) ? kChainBelKey : 0)
                  : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes, it.d.slab_r)
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2)
-                 : b.simple ? variant_key(kMaxIn, 1, 1)         // the widest input class runs any input count
-                            : variant_key(it.d.n_in, it.d.v1, it.d.v2);
+                 : (b.simple ? variant_key(kMaxIn, 1, 1)        // the widest input class runs any input count
+                             : variant_key(it.d.n_in, it.d.v1, it.d.v2)) +
+                       (generic_o32(max_in_bytes(b)) ? kGenericO32 : 0);
     });
     const double T2 = clk();
     for (const Item &it : items)
