@@ -64,6 +64,32 @@ __device__ __forceinline__ vec_t<T, W> pack_vec(const T *x) {
     for (int k = 0; k < W; ++k) v[k] = x[k];
     return v;
 }
+// max of two non-negative, non-NaN values: one v_max (a compare and select
+// otherwise, for NaN semantics that cannot arise here)
+template <typename T>
+__device__ __forceinline__ T max_nn(T a, T b) {
+    if constexpr (sizeof(T) == 4) return __builtin_fmaxf(a, b);
+    else return __builtin_fmax(a, b);
+}
+// entry `lane` of a run starting at the uniform address `base`, as a scalar
+// base plus a 32-bit vector byte offset (the saddr form of global_load /
+// global_store): the base is pinned to scalar registers (readfirstlane of its
+// halves) and the offset is made opaque in the accessing block (instruction
+// selection works block by block; a loop-invariant offset hoisted out of the
+// loop arrives as a 64-bit value and every access gets a 64-bit vector
+// address add)
+__device__ __forceinline__ uint32_t lane_bytes(int lane, int eb) {
+    uint32_t o;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(o) : "v"((uint32_t)lane * (uint32_t)eb));
+    return o;
+}
+template <typename T>
+__device__ __forceinline__ T *lane_at(T *base, uint32_t lane_off) {
+    const uint64_t v = (uint64_t)base;
+    const uint64_t u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return (T *)((char *)u + lane_off);
+}
 template <typename T>
 __device__ __forceinline__ T pow2_t(int e) {
     if constexpr (sizeof(T) == 4) return __builtin_amdgcn_ldexpf(1.0f, e);
@@ -96,27 +122,51 @@ __device__ __forceinline__ void split_step(T (&t)[16], const T *gp, Digit &&digi
         g[q][1][0] = v[2];
         g[q][1][1] = v[3];
     }
+    auto gv = [&](int q, int n, int x) { return NQ == 2 && q ? g[NQ - 1][n][x] : g[0][n][x]; };
+    // acc = 0; acc += G(0, n) m0; acc += G(1, n) m1 for n = 0, 1.  0 + p == p
+    // exactly for the non-negative p of a potential table (no -0 can arise),
+    // so the leading add is dropped.
+    if constexpr (sizeof(T) == 4) {
+        // packed pairs: entries e and e | 1 are one register pair throughout
+        // (no moves to pair them up per bucket).  The bucket whose slot sits
+        // at bit 0 has both its inputs in one pair; every other bucket takes
+        // two pairs, {e, e|1} (x = 0) and {e|PJ, e|PJ|1} (x = 1), to two.
+        // Each entry's products and sum are the scalar ones, in that order.
+        if constexpr (PJ == 1) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        if (e & PJ) continue;
-        const int q = HASQ ? digit(e, HASQ ? Q : 0) : 0;    // constant for local slots
-        const T g00 = NQ == 2 && q ? g[NQ - 1][0][0] : g[0][0][0];
-        const T g10 = NQ == 2 && q ? g[NQ - 1][0][1] : g[0][0][1];
-        const T g01 = NQ == 2 && q ? g[NQ - 1][1][0] : g[0][1][0];
-        const T g11 = NQ == 2 && q ? g[NQ - 1][1][1] : g[0][1][1];
-        // acc = 0; acc += G(0, n) m0; acc += G(1, n) m1 for n = 0, 1 (fp32:
-        // packed pairs).  0 + p == p exactly for the non-negative p of a
-        // potential table (no -0 can arise), so the leading add is dropped.
-        if constexpr (sizeof(T) == 4) {
-            const v2f m0 = {t[e], t[e]}, m1 = {t[e | PJ], t[e | PJ]};
-            const v2f gx0 = {g00, g01}, gx1 = {g10, g11};
-            const v2f p0 = gx0 * m0, p1 = gx1 * m1;
-            const v2f a = p0 + p1;
-            t[e] = a[0];
-            t[e | PJ] = a[1];
+            for (int e = 0; e < 16; e += 2) {
+                const int q = HASQ ? digit(e, HASQ ? Q : 0) : 0;
+                const v2f a = {t[e], t[e | 1]};
+                const v2f m0 = __builtin_shufflevector(a, a, 0, 0), m1 = __builtin_shufflevector(a, a, 1, 1);
+                const v2f gx0 = {gv(q, 0, 0), gv(q, 1, 0)}, gx1 = {gv(q, 0, 1), gv(q, 1, 1)};
+                const v2f p0 = gx0 * m0, p1 = gx1 * m1;
+                const v2f r = p0 + p1;
+                t[e] = r[0];
+                t[e | 1] = r[1];
+            }
         } else {
+#pragma unroll
+            for (int e = 0; e < 16; e += 2) {
+                if (e & PJ) continue;
+                const int qa = HASQ ? digit(e, HASQ ? Q : 0) : 0, qb = HASQ ? digit(e | 1, HASQ ? Q : 0) : 0;
+                const v2f a = {t[e], t[e | 1]}, c = {t[e | PJ], t[e | PJ | 1]};
+                const v2f g00 = {gv(qa, 0, 0), gv(qb, 0, 0)}, g10 = {gv(qa, 0, 1), gv(qb, 0, 1)};
+                const v2f g01 = {gv(qa, 1, 0), gv(qb, 1, 0)}, g11 = {gv(qa, 1, 1), gv(qb, 1, 1)};
+                const v2f pa0 = g00 * a, pa1 = g10 * c, pc0 = g01 * a, pc1 = g11 * c;
+                const v2f ra = pa0 + pa1, rc = pc0 + pc1;
+                t[e] = ra[0];
+                t[e | 1] = ra[1];
+                t[e | PJ] = rc[0];
+                t[e | PJ | 1] = rc[1];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            if (e & PJ) continue;
+            const int q = HASQ ? digit(e, HASQ ? Q : 0) : 0;    // constant for local slots
             const T m0 = t[e], m1 = t[e | PJ];
-            const T p00 = g00 * m0, p01 = g01 * m0, p10 = g10 * m1, p11 = g11 * m1;
+            const T p00 = gv(q, 0, 0) * m0, p01 = gv(q, 1, 0) * m0, p10 = gv(q, 0, 1) * m1, p11 = gv(q, 1, 1) * m1;
             t[e] = p00 + p10;
             t[e | PJ] = p01 + p11;
         }
@@ -154,10 +204,16 @@ struct SplitState {
 };
 
 template <typename T, int F, int DEP, bool DENSE, int FORM>
-__device__ __forceinline__ void split_load_state(SplitState<T, F, DEP> &c, const BucketDesc &d, const int64_t *pool,
-                                                 TableMeta *meta, int w) {
+__device__ __forceinline__ void split_load_state(SplitState<T, F, DEP> &c, cst_t<BucketDesc> &d, const int64_t *pool_,
+                                                 TableMeta *meta_, int w) {
+    // descriptor, dims pool and table pointers through the scalar cache (they
+    // are read-only while the run executes): the state is uniform, and read
+    // with vector loads it would sit in vector registers, making every tile's
+    // address arithmetic 64-bit vector work
+    cst_t<int64_t> *pool = as_const(pool_);
+    cst_t<TableMeta> *meta = as_const(meta_);
     constexpr int HB = 8 - F;
-    c.dims = pool;
+    c.dims = pool_;
     c.n_dims = d.n_dims;
     c.n_tiles = d.n_tiles;
     c.t0h = d.tdiv0[0];
@@ -165,7 +221,7 @@ __device__ __forceinline__ void split_load_state(SplitState<T, F, DEP> &c, const
     c.gmask = (d.chain >> 8) & 0xff;
     c.flags = d.flags;
     c.in_base = d.in_base[0];
-    const int64_t *sl = pool + (int64_t)d.n_dims * (4 + F);
+    cst_t<int64_t> *sl = pool + (int64_t)d.n_dims * (4 + F);
     c.isw = 0;
     c.osw = 0;
 #pragma unroll
@@ -180,7 +236,7 @@ __device__ __forceinline__ void split_load_state(SplitState<T, F, DEP> &c, const
     }
     if constexpr (DENSE) {
         c.d_shift = __builtin_ctz((uint32_t)((uint64_t)pool[0] & 0xffffffffu)) - 6;     // card0 / 64 tiles per row
-        const int64_t *r1 = pool + (4 + F);
+        cst_t<int64_t> *r1 = pool + (4 + F);
         const bool two = d.n_dims == 2;
         c.d_in1 = two ? r1[2] : 0;
         c.d_out1 = two ? r1[3] : 0;
@@ -188,7 +244,7 @@ __device__ __forceinline__ void split_load_state(SplitState<T, F, DEP> &c, const
         for (int j = 0; j < F; ++j) c.d_g1[j] = two ? (int32_t)r1[4 + j] : 0;
         c.d_slab = FORM == kChainFwd ? sl[2 * (F - 1)] : sl[1];          // is[F-1] / os[0]
     }
-    const int64_t *st = sl + 2 * F;
+    cst_t<int64_t> *st = sl + 2 * F;
     int gi = 1;
 #pragma unroll
     for (int j = 0; j < F; ++j) {
@@ -263,7 +319,10 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     T *xch = reinterpret_cast<T *>(dyn + kRedBytes);
     unsigned char *img = dyn + kRedBytes + split_xch_bytes(F, EB);
     T *small = reinterpret_cast<T *>(dyn + kRedBytes + split_xch_bytes(F, EB) + split_img_bytes(F, EB));
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // the wave id as a uniform (scalar) value: derived from threadIdx the
+    // compiler takes it as varying per lane, and everything computed from it
+    // (slab bases, digits) would occupy vector registers and instructions
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // digit of slot p (4 <= p < F) in phase 1: bit (F-1-p) of w
     auto wdig = [&](int p) { return (w >> (F - 1 - p)) & 1; };
     // the tile's 64 rows are 64 * N * EB contiguous bytes; row traffic
@@ -287,7 +346,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         cur = bi;
         cur_begin = d.vblk_begin;
         cur_end = bi + 1 < n_desc ? descs[bi + 1].vblk_begin : total_vblocks;
-        split_load_state<T, F, DEP, DENSE, FORM>(c, d, pool + d.dim_off, meta, w);
+        split_load_state<T, F, DEP, DENSE, FORM>(c, *as_const(descs + bi), pool + d.dim_off, meta, w);
         int fs[kMaxDescIn];
         c.left = chain_fold<T>(d, meta, fs);
         // exp2 of the output: the inputs' exp2 and max exponents, plus the
@@ -377,19 +436,21 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     // the tile's message loads (16 values per lane)
     auto issue = [&](int64_t in_off, T (&rg)[16]) {
         if constexpr (DENSE && FORM == kChainFwd) {
-            // slab x = (slots 0-3 = e) << (F - 4) | (slots 4.. = w), at x * S
-            const T *wb = c.big + tin + (int64_t)w * c.d_slab + lane;
+            // slab x = (slots 0-3 = e) << (F - 4) | (slots 4.. = w), at x * S:
+            // uniform slab bases plus the lane's 32-bit byte offset
+            const T *wb = c.big + tin + (int64_t)w * c.d_slab;
             const int64_t step = c.d_slab << (F - 4);
+            const uint32_t lo = lane_bytes(lane, EB);
 #pragma unroll
-            for (int e = 0; e < 16; ++e) rg[e] = gload(wb + e * step);
+            for (int e = 0; e < 16; ++e) rg[e] = gload(lane_at(wb + e * step, lo));
         } else if constexpr (DENSE) {
             // 64 input rows of N contiguous values at tin + row * N
+            // (the rows are contiguous: chunk q at VE q; uniform part + lane)
             const T *big = c.big + tin;
+            const uint32_t lo = lane_bytes(lane, 16);
 #pragma unroll
             for (int it = 0; it < IT; ++it) {
-                const int q = chunk(it);
-                const int rw = q / CPR, ch = q % CPR;
-                const vec_t<T, VE> v = vload<VE, kNtLoad, true>(big + (int64_t)rw * N + VE * ch);
+                const vec_t<T, VE> v = vload<VE, kNtLoad, true>(lane_at(big + VE * (it * 64 * W + 64 * w), lo));
 #pragma unroll
                 for (int k = 0; k < VE; ++k) rg[VE * it + k] = v[k];
             }
@@ -474,9 +535,10 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     T lv[16];
     auto load_lam = [&](int64_t to) {
         if constexpr (FORM == kChainBwd && DENSE) {
-            const T *lb = c.lam + to + (int64_t)slab_w() * c.d_slab + lane;
+            const T *lb = c.lam + to + (int64_t)slab_w() * c.d_slab;
+            const uint32_t lo = lane_bytes(lane, EB);
 #pragma unroll
-            for (int e = 0; e < 16; ++e) lv[e] = gload(lb + (int64_t)slab_e(e) * c.d_slab);
+            for (int e = 0; e < 16; ++e) lv[e] = gload(lane_at(lb + (int64_t)slab_e(e) * c.d_slab, lo));
         }
     };
     // BM (belief mode): 0 = the run forms no belief; 1 = it does and the
@@ -545,7 +607,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         // (no per-tile rescale: it is folded into the G tables, SplitState)
 #pragma unroll
         for (int e = 0; e < 16; ++e)
-            lmax = t[e] > lmax ? t[e] : lmax;                                  // entries are >= 0, never NaN
+            lmax = max_nn(lmax, t[e]);                     // entries are >= 0, never NaN
 
         if constexpr (FORM == kChainFwd) {
             // row position of entry e: w * 16 + e (slot 0 most significant)
@@ -557,13 +619,14 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             // the 64 rows are one contiguous block of 64 * N entries (planner-checked):
             // 1 KiB per wave-instruction (chunk())
             T *out = c.out + (DENSE ? tout : __shfl(out_off, 0, 64));
+            const uint32_t lo = lane_bytes(lane, 16);
             // (tiles are whole: the planner requires rest dim 0 to be a multiple of 64)
 #pragma unroll
             for (int it = 0; it < IT; ++it) {
                 const int q = chunk(it);                   // 16-B chunk within the block
                 const int rw = q / CPR, ch = q % CPR;
                 const vec_t<T, VE> v = *reinterpret_cast<const vec_t<T, VE> *>(img + rw * ROWB + 16 * ch);
-                vstore<VE, kNtStore, true>(out + VE * (int64_t)q, v);
+                vstore<VE, kNtStore, true>(lane_at(out + VE * (int64_t)(it * 64 * W + 64 * w), lo), v);
             }
         } else {
             // slab stores: entry e has n-digits 0-3 = (w << HB | h), slots 4.. = sc
@@ -571,9 +634,11 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 // output slab of n-digits (slot p at S << p): e's local bits are
                 // slots 4-HB .. F-1 (MSB first), the wave's digits the others
                 const int wsl = slab_w();
-                T *wb = c.out + tout + (int64_t)wsl * c.d_slab + lane;
+                T *wb = c.out + tout + (int64_t)wsl * c.d_slab;
+                const uint32_t lo = lane_bytes(lane, EB);
 #pragma unroll
-                for (int e = 0; e < 16; ++e) store_n<T, 1, kNtStore, true>(wb + (int64_t)slab_e(e) * c.d_slab, &t[e]);
+                for (int e = 0; e < 16; ++e)
+                    store_n<T, 1, kNtStore, true>(lane_at(wb + (int64_t)slab_e(e) * c.d_slab, lo), &t[e]);
                 if (BM == 1 || (BM == 2 && c.bel)) {
                     // belief of rest entry r = lane: lam * pi per slab s into row r
                     // of the image (free: every wave read its rows before the
