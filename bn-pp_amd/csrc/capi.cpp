@@ -147,6 +147,9 @@ int run_single(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &c
             span += sat_mul(cards[v.vars[j]] - 1, v.strides[j]);
         a.meta[i].size = span;
     }
+    // BNPP_NO_O32=1 (tests): claim a span that rules out the 32-bit-offset kernels
+    if (const char *no32 = std::getenv("BNPP_NO_O32"); no32 && *no32 == '1')
+        for (size_t i = 0; i < in_ptrs.size(); ++i) a.meta[i].size = (int64_t)1 << 40;
     a.meta[in_ptrs.size()].ptr = out;
     if (a.d.big >= 0) {
         const int eb = dtype == BNPP_F32 ? 4 : 8;

@@ -2493,6 +2493,9 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
     for (const Item &it : items) ++lvl_n[it.level];
     const char *ns = tuning_knob("BNPP_NO_SIMPLE_LEVELS");
     const bool simplify = !(ns && *ns == '1');
+    // BNPP_NO_O32=1: generic kernels with 64-bit offsets only (tests compare the two bit for bit)
+    const char *no32 = std::getenv("BNPP_NO_O32");
+    const bool no_o32 = no32 && *no32 == '1';
     parallel_for((int64_t)items.size(), [&](int64_t idx) {
         Item &it = items[idx];
         BucketSpec b = *it.b;
@@ -2525,7 +2528,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2)
                  : (b.simple ? variant_key(kMaxIn, 1, 1)        // the widest input class runs any input count
                              : variant_key(it.d.n_in, it.d.v1, it.d.v2)) +
-                       (generic_o32(max_in_bytes(b)) ? kGenericO32 : 0);
+                       (generic_o32(max_in_bytes(b)) && !no_o32 ? kGenericO32 : 0);
     });
     const double T2 = clk();
     for (const Item &it : items)

@@ -29,7 +29,7 @@ constexpr const char *kPlanKnobs[] = {"BNPP_NO_CHAIN", "BNPP_NO_SPLIT", "BNPP_NO
                                       "BNPP_NO_SLAB_OUTER", "BNPP_NO_BEL_FUSE", "BNPP_NO_CHAIN_FWDV",
                                       "BNPP_NO_FREE_REDUCE", "BNPP_NO_REDUCE_MANY", "BNPP_NO_DEDUP",
                                       "BNPP_TREE_SLOTS", "BNPP_KEEP_LOG2", "BNPP_SLOW_LOG2", "BNPP_SPLIT_MIN_F",
-                                      "BNPP_CHAIN_RUN_MAX", "BNPP_MEM_BUDGET_GB"};
+                                      "BNPP_CHAIN_RUN_MAX", "BNPP_MEM_BUDGET_GB", "BNPP_NO_O32"};
 
 // Run body(i) for i in [0, n) on up to `threads` host threads (0: hardware
 // concurrency, capped at 16 — the per-GPU CPU share of the target machines).

@@ -649,3 +649,37 @@ def test_model_free_releases_cached_job_and_sources(ctx):
     z2 = bnpp.partition(ctx, m2, {}, "mf", bnpp.F64)[1]
     assert bnpp.last_timing()["plan_ms"] > 0.0             # a new model: planned afresh
     assert z == z2 == refcpu.Model.from_dict(d).partition({}, "mf")[0]
+
+
+def test_generic_offsets_32_and_64_bit_identical(ctx, monkeypatch):
+    """The generic gather kernels take 32-bit table offsets when every input
+    of a launch is under 4 GiB (kGenericO32) and 64-bit ones otherwise;
+    BNPP_NO_O32=1 forces the 64-bit kernels everywhere.  Same bits either way:
+    PRs whose largest buckets are whole-dim odd tiles (Munin1: card-7 rows),
+    a corpus network with evidence, per-target marginals, and random single
+    buckets against the oracle."""
+    cases = [("Munin1.uai", None), ("Pigs.uai", "Pigs.uai.evid"), ("alarm.uai", "alarm.uai.evid")]
+    runs = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("BNPP_NO_O32", flag)
+        out = []
+        for name, evn in cases:
+            m = bnpp.Model.load(model_path(name))
+            ev = evidence_of(evn) if evn else {}
+            for dt in (bnpp.F64, bnpp.F32):
+                out.append(bnpp.partition(ctx, m, ev, "mf", dt)[:2])
+        m = bnpp.Model.load(model_path("alarm.uai"))
+        out.append(bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)[0])
+        rng = random.Random(77)
+        for it in range(40):
+            cards, ins, elim = _rand_bucket(rng)
+            scope, vals, psum = run_bucket(ctx, bnpp.F64, cards, ins, elim, with_sum=True)
+            fs = [refcpu.Factor.new(s, cards, v) for s, v in ins]
+            ref = refcpu.bucket(fs, elim, cards[elim]) if elim >= 0 else fs[0]
+            if elim < 0:
+                for f in fs[1:]:
+                    ref = ref.product(f)
+            assert vals == ref.values, (flag, it)
+            out.append((scope, vals, psum))
+        runs[flag] = out
+    assert runs["0"] == runs["1"]
