@@ -637,8 +637,15 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         }
         const int eb = max_vec == 2 ? 8 : 4;
         const char *off = tuning_knob("BNPP_NO_STREAM");
+        // a fastest output dim of card 3, 5, 6 or 7 leaves the stream form at
+        // 1x1 tiles (a decode over every dim per output); the generic kernel's
+        // whole-dim tiles (below) serve it instead
+        const uint64_t c0 = merged.empty() ? 0 : merged[0].card;
+        const char *os = tuning_knob("BNPP_ODD_STREAM");                 // A/B knob: 1 = keep the stream form
+        const bool odd_rows = v1 == 1 && (c0 == 3 || c0 == 5 || c0 == 7 || (c0 == 6 && aligned(0, 2))) && (int)c0 <= max_tile &&
+                              !(os && *os == '1');
         if (!b.simple && !b.divide && n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 &&
-            !(off && *off == '1')) {
+            !(off && *off == '1') && !odd_rows) {
             int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
             int64_t s1 = merged.size() < 2 ? 0 : merged[1].s[big];
             // slab form (slab.cuh): the big input is k slabs contiguous along the
