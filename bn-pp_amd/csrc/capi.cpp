@@ -355,8 +355,11 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                 if (ev[v] < 0) vars.push_back(v);
             max_width = elimination_order(nv, d.cards, scopes, vars, (Heuristic)heuristic, ord);
         }
+        const bool tt = std::getenv("BNPP_TIMING") != nullptr;
+        double tq = now_ms();
         plans.push_back(plan_bucket_tree(d.cards, views, ord, targets, part, n_parts));
         auto need = [&](const VEPlan &p) { return sat_add(plan_arena_bytes(p, eb), (int64_t)p.buckets.size() * 512); };
+        if (tt) std::fprintf(stderr, "[bnpp] bucket tree: tree plan %.1f ms\n", now_ms() - tq);
         const char *force = std::getenv("BNPP_TREE_SLOTS");     // testing / tuning: chain mode, fixed slots
         if (force && std::atoi(force) > 0) {
             std::string msg;
@@ -365,7 +368,8 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                                         n_slices, slice_rank, false, eb))
                 return set_err(BNPP_ERR_UNSUPPORTED, msg);
             plans.back() = std::move(cp);
-        } else if (need(plans.back()) > budget || n_parts > 1 || n_slices > 1) {
+        } else if ((tq = now_ms(), need(plans.back()) > budget) || n_parts > 1 || n_slices > 1) {
+            if (tt) std::fprintf(stderr, "[bnpp] bucket tree: whole-tree need %.1f ms\n", now_ms() - tq);
             // every forward message does not fit: recompute them from checkpoints
             // (chain-shaped trees), with as many checkpoint slots as fit
             std::string msg;
@@ -409,6 +413,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             // probes planned in parallel per round (two rounds for 64 counts
             // instead of six bisection steps; a cold call's planning time)
             while (lo <= hi && exact) {
+                tq = now_ms();
                 const int m = hi - lo + 1, n = std::min(8, m);
                 std::vector<int> probe(n);                // ascending, inside [lo, hi]
                 for (int i = 0; i < n; ++i) probe[i] = m <= 8 ? lo + i : lo + (int)((int64_t)m * (i + 1) / (n + 1));
@@ -444,6 +449,7 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                 }
                 lo = new_lo;
                 hi = new_hi;
+                if (tt) std::fprintf(stderr, "[bnpp] bucket tree: %d slot probes %.1f ms\n", n, now_ms() - tq);
             }
             if (best_s > 0) {
                 if (best_s != memo_s && exact) {
