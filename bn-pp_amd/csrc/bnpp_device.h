@@ -30,10 +30,15 @@ constexpr int kSplitPack = 8;
 constexpr int kSplitLdsBytes = 160 * 1024;
 constexpr int split_xch_bytes(int f, int eb = 4) { return kSplitRowsHost * (1 << f) * eb; }
 constexpr int split_img_bytes(int f, int eb = 4) { return kSplitRowsHost * ((1 << f) * eb + 16); }
+// fp64 runs of 8 exist only as kernels whose row image shares the exchange
+// table's LDS (chainsplit.cuh split_alias): the larger of the two, not the sum
 constexpr int split_g_budget_bytes(int f, int eb = 4) {
-    return kSplitLdsBytes - 64 - split_xch_bytes(f, eb) - split_img_bytes(f, eb);
+    return kSplitLdsBytes - 64 -
+           (eb == 8 && f == 8 ? (split_xch_bytes(f, eb) > split_img_bytes(f, eb) ? split_xch_bytes(f, eb) : split_img_bytes(f, eb))
+                              : split_xch_bytes(f, eb) + split_img_bytes(f, eb));
 }
-constexpr int split_max_f(int eb) { return eb == 4 ? 8 : 7; }    // longest split run per element size
+constexpr int split_max_f(int eb) { return eb == 4 ? 8 : 8; }    // longest split run per element size
+constexpr int split_max_bel_f(int eb) { return eb == 4 ? 8 : 7; } // longest run forming a fused belief
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 
 // One per table (source factor or message), resident in device memory.

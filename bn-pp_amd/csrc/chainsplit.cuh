@@ -1,8 +1,8 @@
 // Split chain runs (gfx950): F consecutive sweep buckets of a binary (K = 2)
 // message fused in one pass, the 2^F-entry table of one rest entry spread
-// over W = 2^(F-4) waves of one workgroup (16 entries per lane): F = 5..8 in
-// fp32, 5..7 in fp64 (an fp64 run of 8 would need a 128-KiB exchange table
-// beside its 129-KiB row image; 160 KiB of LDS hold both only up to F = 7).
+// over W = 2^(F-4) waves of one workgroup (16 entries per lane): F = 5..8
+// (an fp64 run of 8 has a 128-KiB exchange table and a 129-KiB row image:
+// they share their LDS, split_alias, and such runs form no fused belief).
 //
 // Same arithmetic as chain.cuh (one thread per rest entry, all 2^F entries in
 // its registers), which caps a run at 6 buckets (64 registers of table, 3 waves
@@ -106,6 +106,9 @@ __host__ __device__ constexpr int split_waves(int f) { return 1 << (f - 4); }
 // any slot's digit for entry e (local ones from e, the others wave-uniform).
 template <typename T, int F, int PH, int J, int DEP, typename Digit>
 __device__ __forceinline__ void split_step(T (&t)[16], const T *gp, Digit &&digit) {
+#ifdef BNPP_PROBE_NO_ARITH
+    if constexpr (sizeof(T) == 8) { (void)gp; (void)digit; asm volatile("" : "+v"(t[0])); return; }
+#endif
     // place of slot J in the local index
     constexpr int PJ = PH == 1 ? (8 >> J) : (1 << (F - 1 - J));
     constexpr int Q = DEP == kDepNext ? J + 1 : J - 1;
@@ -288,12 +291,30 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // without a belief to that many waves per SIMD (4: 128 VGPRs, the persistent
 // grid's 16 waves per CU, at the price of a few spilled registers; left
 // alone they take 128-164 VGPRs, 3 waves)
-#ifndef BNPP_F64_SPLIT_WAVES
-#define BNPP_F64_SPLIT_WAVES 1
+//
+// fp64 one-run kernels without a belief (MODE 0) alias the row image with the
+// exchange table (split_alias): 65 KiB of LDS per workgroup instead of 129,
+// so two 8-wave workgroups share a CU, at two more barriers per tile (the
+// image's reads and the exchange's must finish before the other is written);
+// the next tile's loads wait in registers instead of the exchange slots, and
+// the registers are held to 128 (four waves per SIMD).
+#ifndef BNPP_F64_ALIAS
+#define BNPP_F64_ALIAS 1
 #endif
+// (fp64 runs of 8 need it in every kernel they have: one-run and multi-run;
+// they form no fused belief, so there is no MODE 1 kernel of them)
+template <typename T, int MODE, int F>
+__host__ __device__ constexpr bool split_alias() {
+    return sizeof(T) == 8 && (((BNPP_F64_ALIAS != 0 || F == 8) && MODE == 0) || (F == 8 && MODE == 2));
+}
+template <int F, int EB, bool ALIAS>
+__host__ __device__ constexpr int split_tile_lds() {
+    return ALIAS ? (split_xch_bytes(F, EB) > split_img_bytes(F, EB) ? split_xch_bytes(F, EB) : split_img_bytes(F, EB))
+                 : split_xch_bytes(F, EB) + split_img_bytes(F, EB);
+}
 template <typename T, int F, int FORM, int DEP, bool DENSE, int MODE>
 __global__ __launch_bounds__(64 * (1 << (F - 4)))
-__attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 && DENSE && MODE == 0 ? BNPP_F64_SPLIT_WAVES : 1)))
+__attribute__((amdgpu_waves_per_eu(split_alias<T, MODE, F>() ? 4 : 1)))
 void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const int64_t *__restrict__ pool,
                         TableMeta *__restrict__ meta, int64_t total_vblocks) {
     constexpr int EB = sizeof(T);
@@ -305,20 +326,24 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
     constexpr int HB = 8 - F;                              // phase 2: bits of h (n-digits 0-3 local)
     constexpr int SB = F - 4;                              // phase 2: bits of the slot combo (slots 4..F-1)
     constexpr int CPR = N * EB / 16;                       // 16-B chunks per row
-    static_assert(W * EB <= kRedBytes, "reduction scratch");
-    static_assert(EB == 4 || F <= 7, "fp64 split runs: F <= 7 (LDS)");
+
     // fp64: the row image and exchange table leave room for one workgroup
     // (8 waves at F = 7) per CU, so forward runs keep two tiles' loads in
     // flight instead of one (2 waves per SIMD: the registers are there):
     // 17.08 -> 16.34 ms per 2^32-entry message; the backward runs got slower
     // that way (17.12 -> 17.57 ms) and keep one, and so did fp32 forward runs
     // at 16 waves per CU (5.99 -> 6.23 ms; profiles/r05_f64_ahead2.txt)
-    constexpr bool AHEAD2 = EB == 8;
+    constexpr bool ALIAS = split_alias<T, MODE, F>();
+    constexpr bool AHEAD2 = EB == 8 && !ALIAS;
+    static_assert(EB == 4 || F <= 7 || ALIAS, "fp64 split runs of 8: the aliased LDS layout only");
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
-    T *red = reinterpret_cast<T *>(dyn);
+    // the per-wave maxima at a flush: the reduction scratch, or (16 fp64
+    // waves) the start of the tile region, free there -- flush() waits for
+    // every wave first, and what follows it (setup) waits before LDS is reused
+    T *red = reinterpret_cast<T *>(W * EB <= kRedBytes ? dyn : dyn + kRedBytes);
     T *xch = reinterpret_cast<T *>(dyn + kRedBytes);
-    unsigned char *img = dyn + kRedBytes + split_xch_bytes(F, EB);
-    T *small = reinterpret_cast<T *>(dyn + kRedBytes + split_xch_bytes(F, EB) + split_img_bytes(F, EB));
+    unsigned char *img = dyn + kRedBytes + (ALIAS ? 0 : split_xch_bytes(F, EB));
+    T *small = reinterpret_cast<T *>(dyn + kRedBytes + split_tile_lds<F, EB, ALIAS>());
     // the wave id as a uniform (scalar) value: derived from threadIdx the
     // compiler takes it as varying per lane, and everything computed from it
     // (slab bases, digits) would occupy vector registers and instructions
@@ -586,6 +611,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             split_step<T, F, 1, j, DEP>(t, small + c.glds[j] + gb[j] * kSplitPack, dig1);
         });
         // exchange: entry (n-digits 0-3 = e, slots 4.. = w) -> xch[(w * 16 + e) * 64 + lane]
+        if constexpr (ALIAS) lds_barrier();                // every wave's image reads are done
 #pragma unroll
         for (int e = 0; e < 16; ++e) xch[(w * 16 + e) * 64 + lane] = t[e];
         lds_barrier();
@@ -595,6 +621,8 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             const int h = e >> SB, sc = e & ((1 << SB) - 1);
             t[e] = xch[(sc * 16 + ((w << HB) | h)) * 64 + lane];
         }
+        // (forward: the image write below; backward: the next tile's image write)
+        if constexpr (ALIAS) lds_barrier();                // every wave's exchange reads are done
         auto dig2 = [&](int e, int p) {
             if (p >= 4) return (e >> (F - 1 - p)) & 1;
             const int cg = (w << HB) | (e >> SB);
@@ -741,6 +769,27 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
 #pragma unroll
             for (int e = 0; e < 16; ++e) xch[(w * 16 + e) * 64 + lane] = p[e];
         };
+        if constexpr (ALIAS) {
+            // fp64 with the image on the exchange table: the next tile's loads
+            // wait in registers (two sets in turn, the loop unrolled twice, so
+            // no set is copied at the latch)
+            T pa[16], pb[16];
+            decode(vb, in_off, out_off, gb);
+            issue(in_off, pa);
+            auto step = [&](T (&cur)[16], T (&nxt)[16]) {
+                const int64_t vbn = vb + gridDim.x;
+                decode(vbn < last ? vbn : last, in_off, out_off, gb);
+                issue(in_off, nxt);
+                decode(vb, in_off, out_off, gb);
+                run_tile(std::integral_constant<int, 0>{}, cur, out_off, gb);
+                vb = vbn;
+                return vb < total_vblocks;
+            };
+            while (step(pa, pb) && step(pb, pa)) {
+            }
+            flush();
+            return;
+        }
         if constexpr (AHEAD2) {
             // fp64: the tile after next is loaded while this one is computed
             // (two register sets in turn, a loop unrolled twice); the next
@@ -814,7 +863,10 @@ template <typename T, int F, int FORM, int DEP, bool DENSE, bool BEL>
 static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_t stream) {
     constexpr int EB = sizeof(T);
     constexpr int MODE1 = BEL ? 1 : 0;                    // one-run kernel of this key
-    const size_t shm = kRedBytes + split_xch_bytes(F, EB) + split_img_bytes(F, EB) + (size_t)small_elems * EB;
+    const bool one = a.n_desc == 1;
+    const bool alias = one ? split_alias<T, MODE1, F>() : split_alias<T, 2, F>();
+    const size_t tile_lds = alias ? split_tile_lds<F, EB, true>() : split_tile_lds<F, EB, false>();
+    const size_t shm = kRedBytes + tile_lds + (size_t)small_elems * EB;
     // per device (a process may drive several): the 160-KiB LDS opt-in of
     // this instantiation and the CU count the persistent grid is sized for
     struct DevState {
@@ -848,7 +900,7 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     int per_cu = BNPP_SPLIT_WAVES_PER_CU / split_waves(F) > 0 ? BNPP_SPLIT_WAVES_PER_CU / split_waves(F) : 1;
     per_cu = std::max(1, std::min<int>(per_cu, (int)((size_t)kSplitLdsBytes / shm)));
     const int64_t grid = a.vblocks < (int64_t)cus * per_cu ? a.vblocks : (int64_t)cus * per_cu;
-    if (a.n_desc == 1)
+    if (one)
         hipLaunchKernelGGL((chain_split_kernel<T, F, FORM, DEP, DENSE, MODE1>), dim3((unsigned)grid),
                            dim3(64 * split_waves(F)), shm, stream, a.descs, a.n_desc, a.pool, a.meta, a.vblocks);
     else
@@ -858,8 +910,8 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
 }
 
 // forms kChainFwdS / kChainBwdS and their dense variants kChainFwdSD /
-// kChainBwdSD (bnpp_device.h), K = 2, dep next / prev; F = 5..8 (fp32),
-// 5..7 (fp64); dense backward runs forming a fused belief have their own key
+// kChainBwdSD (bnpp_device.h), K = 2, dep next / prev; F = 5..8 (fp64 runs of
+// 8 without a belief kernel); dense backward runs forming a fused belief have their own key
 // (chain_key + kChainBelKey)
 #define BNPP_CASE_CHAIN_SPLIT(T, F, FORM, KFORM, DEP, DENSE, BEL) \
     case 8192 + DEP * 2048 + FORM * 256 + 2 * 16 + F + (BEL ? kChainBelKey : 0): \
@@ -873,7 +925,12 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     X(T, F, 8, kChainBwd, 0, true, true) X(T, F, 8, kChainBwd, 1, true, true)
 #define BNPP_CHAIN_SPLIT(X) BNPP_CHAIN_SPLIT_FD(X, float, 5) BNPP_CHAIN_SPLIT_FD(X, float, 6) \
     BNPP_CHAIN_SPLIT_FD(X, float, 7) BNPP_CHAIN_SPLIT_FD(X, float, 8)
+// fp64 runs of 8: no fused-belief kernel (the belief's run is at most 7, split_max_bel_f)
+#define BNPP_CHAIN_SPLIT_FD_NOBEL(X, T, F) X(T, F, 5, kChainFwd, 0, false, false) X(T, F, 5, kChainFwd, 1, false, false) \
+    X(T, F, 6, kChainBwd, 0, false, false) X(T, F, 6, kChainBwd, 1, false, false) \
+    X(T, F, 7, kChainFwd, 0, true, false) X(T, F, 7, kChainFwd, 1, true, false) \
+    X(T, F, 8, kChainBwd, 0, true, false) X(T, F, 8, kChainBwd, 1, true, false)
 #define BNPP_CHAIN_SPLIT_F64(X) BNPP_CHAIN_SPLIT_FD(X, double, 5) BNPP_CHAIN_SPLIT_FD(X, double, 6) \
-    BNPP_CHAIN_SPLIT_FD(X, double, 7)
+    BNPP_CHAIN_SPLIT_FD(X, double, 7) BNPP_CHAIN_SPLIT_FD_NOBEL(X, double, 8)
 
 }  // namespace bnpp

@@ -220,8 +220,8 @@ static bool build_chain_desc(const BucketSpec &b, const std::vector<int> &cards,
         if (cards[b.chain_x[j]] != K || (!sum && cards[b.chain_n[j]] != K)) return fail("chain: mixed cardinalities");
         N *= K;
     }
-    // split form (chainsplit.cuh): binary runs of 5..8 (fp32) / 5..7 (fp64)
-    // buckets over 2^(F-4) waves
+    // split form (chainsplit.cuh): binary runs of 5..8 buckets over 2^(F-4)
+    // waves (fp64 runs of 8 without a fused belief)
     const char *nsp = std::getenv("BNPP_NO_SPLIT");
     const char *smf = std::getenv("BNPP_SPLIT_MIN_F");
     const int split_min = smf ? std::max(5, std::atoi(smf)) : 5;
@@ -1865,7 +1865,7 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         auto bel_run = [&](int j) {
             if (sbits != 0 || !multi.count(j) || B.chain_eb == 0) return 0;
             const int f = (int)slow[j].size();
-            return f >= 5 && f <= split_max_f(B.chain_eb) ? f : 0;
+            return f >= 5 && f <= split_max_bel_f(B.chain_eb) ? f : 0;
         };
         auto deliver = [&](int i, const View &lam_j) {
             if (i != next_deliver) return false;

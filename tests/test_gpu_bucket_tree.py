@@ -358,12 +358,13 @@ def test_split_runs_identical_to_unfused(ctx, capfd, spec):
 
 @pytest.mark.parametrize("spec", [(16, 6, None, None), (18, 5, {3: 1, 40: 0}, None), (17, 4, None, 11)])
 def test_split_runs_fp64_identical_to_unfused(ctx, capfd, spec):
-    """fp64 split runs (chainsplit.cuh with T = double: runs of 5..7 buckets,
-    16 entries per lane, scalar fp64 arithmetic in the reference's order):
-    partition and tree marginals bit-identical to the one-thread runs, to one
-    bucket per launch, dense and general addressing alike; the last spec has
-    peaked potentials (every fused run rescales by 2^-50 or more).  The plan
-    holds F = 7 split runs (forms 7, 8 dense; 5, 6 general)."""
+    """fp64 split runs (chainsplit.cuh with T = double: runs of 5..8 buckets,
+    16 entries per lane, scalar fp64 arithmetic in the reference's order; runs
+    of 8 on the aliased LDS layout, split_alias): partition and tree marginals
+    bit-identical to the one-thread runs, to one bucket per launch, dense and
+    general addressing alike; the last spec has peaked potentials (every fused
+    run rescales by 2^-50 or more).  The plan holds F = 8 split runs (forms 7,
+    8 dense; 5, 6 general)."""
     r, c, ev, log2_eps = spec
     ev = ev or {}
     d = synth.ising_grid(r, c, seed=13) if log2_eps is None else synth.peaked_grid(r, c, log2_eps=log2_eps, seed=5)
@@ -386,7 +387,7 @@ def test_split_runs_fp64_identical_to_unfused(ctx, capfd, spec):
         if "BNPP_DEBUG_CHAIN" in kn:
             err = capfd.readouterr().err
             forms = (5, 6) if "BNPP_NO_DENSE" in kn else (7, 8)
-            assert any("run form %d K=2 F=7" % f in err for f in forms), err[-2000:]
+            assert any("run form %d K=2 F=8" % f in err for f in forms), err[-2000:]
     for out in res[1:]:
         assert out == res[0]
     want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
