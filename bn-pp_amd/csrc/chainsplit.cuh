@@ -106,9 +106,6 @@ __host__ __device__ constexpr int split_waves(int f) { return 1 << (f - 4); }
 // any slot's digit for entry e (local ones from e, the others wave-uniform).
 template <typename T, int F, int PH, int J, int DEP, typename Digit>
 __device__ __forceinline__ void split_step(T (&t)[16], const T *gp, Digit &&digit) {
-#ifdef BNPP_PROBE_NO_ARITH
-    if constexpr (sizeof(T) == 8) { (void)gp; (void)digit; asm volatile("" : "+v"(t[0])); return; }
-#endif
     // place of slot J in the local index
     constexpr int PJ = PH == 1 ? (8 >> J) : (1 << (F - 1 - J));
     constexpr int Q = DEP == kDepNext ? J + 1 : J - 1;
