@@ -1862,8 +1862,10 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             }
         };
         // the run length that lets delivery j's belief fuse (attach_belief)
+        const char *nbf = std::getenv("BNPP_NO_BEL_FUSE");
+        const bool bel_fuse = !(nbf && *nbf == '1');
         auto bel_run = [&](int j) {
-            if (sbits != 0 || !multi.count(j) || B.chain_eb == 0) return 0;
+            if (!bel_fuse || sbits != 0 || !multi.count(j) || B.chain_eb == 0) return 0;
             const int f = (int)slow[j].size();
             return f >= 5 && f <= split_max_bel_f(B.chain_eb) ? f : 0;
         };
