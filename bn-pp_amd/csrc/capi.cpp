@@ -412,20 +412,44 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
             // the need grows with the slot count: a k-ary search, up to 8
             // probes planned in parallel per round (two rounds for 64 counts
             // instead of six bisection steps; a cold call's planning time)
+            // first round: eight consecutive counts ending at the estimate
+            // budget / largest message (a checkpoint slot holds one message;
+            // the answer sits a few below it), so that one round usually
+            // brackets the answer and a second is not needed
+            int first_hi = 0;
+            if (lo <= hi && n_slices == 1) {
+                int64_t big = 1;
+                for (const MsgTable &t : plans.back().msgs) big = std::max(big, t.size);
+                const int64_t est = budget / sat_mul(big, eb);
+                if (est >= 1 && est < hi) first_hi = (int)est;
+            }
             while (lo <= hi && exact) {
                 tq = now_ms();
-                const int m = hi - lo + 1, n = std::min(8, m);
+                const int m = hi - lo + 1;
+                int n = std::min(8, m);
                 std::vector<int> probe(n);                // ascending, inside [lo, hi]
                 for (int i = 0; i < n; ++i) probe[i] = m <= 8 ? lo + i : lo + (int)((int64_t)m * (i + 1) / (n + 1));
+                if (first_hi > 0 && m > 8) {
+                    const int k = std::min(n, first_hi);  // first_hi - k + 1 .. first_hi (>= 1)
+                    probe.resize(k);
+                    n = k;
+                    for (int i = 0; i < k; ++i) probe[i] = first_hi - (k - 1) + i;
+                    first_hi = 0;
+                }
                 std::vector<VEPlan> cps(n);
                 std::vector<int64_t> nb(n, 0);
                 std::vector<char> planned(n, 0);
                 std::vector<std::string> msgs(n);
+                std::vector<double> pt(n);
                 parallel_for((int64_t)n, [&](int64_t i) {
+                    const double a = now_ms();
                     planned[i] = plan_bucket_tree_chain(d.cards, views, ord, targets, probe[i], part, n_parts, cps[i],
                                                         &msgs[i], chain_eb, n_slices, slice_rank, false, eb) ? 1 : 0;
                     if (planned[i]) nb[i] = need(cps[i]);
+                    pt[i] = now_ms() - a;
                 });
+                if (tt)
+                    for (int i = 0; i < n; ++i) std::fprintf(stderr, "[bnpp]   probe %d slots: %.1f ms\n", probe[i], pt[i]);
                 int new_lo = lo, new_hi = hi;
                 for (int i = 0; i < n; ++i) {
                     if (!planned[i]) {                    // as a bisection that stops at its first failure

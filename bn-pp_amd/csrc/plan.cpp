@@ -21,8 +21,8 @@ namespace bnpp {
 
 // Persistent host workers (spawning 15 threads per call cost ~1 ms of a
 // millisecond-scale PR plan).  One parallel_for at a time uses the pool; a
-// concurrent or nested call (another context's thread, a body that itself
-// calls parallel_for) runs on threads of its own as before.
+// concurrent call (another context's thread) runs on threads of its own, a
+// nested one (a body that itself calls parallel_for) serially.
 namespace {
 struct HostPool {
     std::mutex run_mu;                         // held by the one call using the pool
@@ -75,7 +75,9 @@ struct HostPool {
             ++gen;
         }
         cv.notify_all();
+        in_worker = true;                      // the caller drains too: its nested calls run serially
         drain();
+        in_worker = false;
         std::unique_lock<std::mutex> lk(mu);
         done_cv.wait(lk, [&] { return active == 0; });
         body = nullptr;
@@ -93,7 +95,11 @@ void parallel_for(int64_t n, const std::function<void(int64_t)> &body, int threa
         if (const char *e = std::getenv("BNPP_HOST_THREADS")) threads = std::atoi(e);
         threads = std::max(1, std::min(threads, 16));
     }
-    if (n <= 1 || threads == 1) {
+    // a body already running on the pool (a worker, or the calling thread
+    // draining with them) loops serially: the pool's threads are busy with
+    // the outer loop, and spawning more per nested call oversubscribes the
+    // host (eight parallel slot probes each splitting their own loops)
+    if (n <= 1 || threads == 1 || HostPool::in_worker) {
         for (int64_t i = 0; i < n; ++i) body(i);
         return;
     }

@@ -5,7 +5,7 @@
 # self-launched two-rank rehearsal.
 set -o pipefail
 R=$PWD
-OUT=$R/gpurun_out/final5b
+OUT=$R/gpurun_out/final5d
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
