@@ -677,3 +677,43 @@ def test_runs_with_non_neighbour_g_fall_back_safely(ctx, rows, cols, hop):
     want, _ = bnpp.marginals(ctx, m, {}, "mf", bnpp.F64)
     for t in range(m.n_vars):
         assert _close(res[0][2][t], want[t], 1e-5), (t, res[0][2][t], want[t])
+
+
+def test_split_runs_fp64_multi_run_levels(ctx, capfd):
+    """A grid cut in two by a column of evidence sweeps both halves at once:
+    the PR has levels holding two fp64 split runs of 8 (one launch, the
+    multi-run kernel on the aliased LDS layout, chainsplit.cuh MODE 2).  Partition and tree
+    marginals bit-identical to one-thread runs and to one bucket per launch;
+    marginals equal per-target VE to 1e-12."""
+    r, c = 16, 13
+    d = synth.ising_grid(r, c, seed=13)
+    m = bnpp.Model.from_dict(d)
+    ev = {i * c + 6: i % 2 for i in range(r)}
+    col = [i * c + j for j in range(c) for i in range(r)]
+    # the PR plan holds levels with two runs of 8 (host-side planning dump)
+    os.environ["BNPP_DUMP_PLAN"] = "1"
+    capfd.readouterr()
+    try:
+        bnpp.plan_stats(m, 0, ev, "mf", dtype=bnpp.F64, order=col)
+    finally:
+        del os.environ["BNPP_DUMP_PLAN"]
+    runs = {}
+    for line in capfd.readouterr().err.splitlines():
+        if " chain F=8 " in line:
+            lvl = line.split()[0]
+            runs[lvl] = runs.get(lvl, 0) + 1
+    assert any(n >= 2 for n in runs.values()), runs
+    res = []
+    for kn in ({}, {"BNPP_NO_SPLIT": "1"}, {"BNPP_NO_CHAIN": "1"}):
+        os.environ.update(kn)
+        try:
+            res.append([bnpp.partition(ctx, m, ev, "mf", bnpp.F64, order=col)[0],
+                        bnpp.marginals_tree(ctx, m, ev, "mf", bnpp.F64, order=col)[0]])
+        finally:
+            for key in kn:
+                del os.environ[key]
+    for out in res[1:]:
+        assert out == res[0]
+    want, _ = bnpp.marginals(ctx, m, ev, "mf", bnpp.F64)
+    for t in range(m.n_vars):
+        assert _close(res[0][1][t], want[t], 1e-12), (t, res[0][1][t], want[t])
