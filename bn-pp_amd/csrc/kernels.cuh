@@ -304,8 +304,8 @@ __device__ __forceinline__ T compute_tile(const LoadedBucketT<NIN> &b, int64_t t
     // leaves one load in flight per thread, and a gather-heavy bucket (Munin1's
     // largest: 3 inputs x 7 values per output) then pays a memory round trip
     // per input and summed value in series.  Unused input slots (i >= n_in)
-    // read entry 0 of input 0 (load_common), so the loads are issued without a
-    // branch per slot.  The arithmetic that follows is unchanged: p = 1;
+    // read entry 0 of the output table (their pointer, set with the others),
+    // so the loads are issued without a branch per slot.  The arithmetic that follows is unchanged: p = 1;
     // p *= in_0; ...; acc += p per summed value in order (factor.cpp:131-143,
     // 199-205).
     constexpr int VB = TS * NIN >= 16 ? 1 : 16 / (TS * NIN);
@@ -548,7 +548,8 @@ __global__ __launch_bounds__(kBlock) void bucket_level_kernel(const BucketDesc *
                         x_sum += mi.exp2;
                     }
                 } else {
-                    b.ptr[i] = b.ptr[0];                   // unused slot: compute_tile reads entry 0
+                    b.ptr[i] = b.out;                      // unused slot: compute_tile reads entry 0 (a
+                                                           // valid address even for a bucket of no inputs)
                 }
             }
             b.neg_e = (int)(-e_sum);
@@ -586,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void bucket_single_kernel(const SingleArgs 
     b.flags = d.flags & kDivide;
     b.neg_e = 0;
     b.out = a.meta[d.n_in].ptr;
-    for (int i = 0; i < NIN; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : a.meta[0].ptr;
+    for (int i = 0; i < NIN; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : b.out;   // unused: entry 0 of the output
     __shared__ __attribute__((aligned(16))) unsigned char lds[(kBlock / 64) * kLdsWaveBytes];
     for (int64_t tid0 = (int64_t)blockIdx.x * kBlock; tid0 < b.n_tiles; tid0 += (int64_t)gridDim.x * kBlock) {
         const int64_t tid = tid0 + threadIdx.x;
