@@ -330,7 +330,7 @@ void chain_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
         if (tid < c.n_tiles) {
             // rest position of this thread: in / out offsets, G offsets in LDS
             const int row = 4 + F;
-            const int64_t *dp = c.dims;
+            cst_t<int64_t> *dp = as_const(c.dims);     // scalar cache: read-only while the launch runs
             int64_t in_off = c.in_base, out_off = 0;
             int32_t gb[F], gv[F];
             uint64_t q, r;

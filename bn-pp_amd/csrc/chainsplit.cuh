@@ -427,7 +427,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         }
         const int64_t tid0 = (vb - cur_begin) * kSplitRows;
         const int row = 4 + F;
-        const int64_t *dp = c.dims;
+        cst_t<int64_t> *dp = as_const(c.dims);          // scalar cache: read-only while the launch runs
         uint64_t q, r;
         divmod_dim((uint64_t)tid0, c.t0h, c.t0m, q, r);
         int64_t ui = c.in_base + (int64_t)r * dp[2], uo = (int64_t)r * dp[3];

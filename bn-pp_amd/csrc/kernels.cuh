@@ -660,7 +660,10 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
     out_off = 0;
     if (b.n_dims > 0) {
         const int row = 2 + b.n_in;
-        const int64_t *os = b.dims + (int64_t)b.n_dims * row;   // kOutStrided: output stride per dim
+        // dims pool through the scalar cache (read-only while the launch
+        // runs): vector loads here would make each tile wait, in vmcnt
+        // order, for the previous tile's stores
+        cst_t<int64_t> *os = as_const(b.dims) + (int64_t)b.n_dims * row;   // kOutStrided: output stride per dim
         uint64_t q, r;
         divmod_dim((uint64_t)tid, b.t0h, b.t0m, q, r);
         int64_t i0 = (int64_t)r * V1;
@@ -675,7 +678,7 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
             for (int i = 0; i < kStreamMaxIn; ++i) pos[i] += i1 * b.s1[i];
             if constexpr (kRows) out_off += i1 * os[1];
             uint64_t rem = q1;
-            const int64_t *dp = b.dims + 2 * row;
+            cst_t<int64_t> *dp = as_const(b.dims) + 2 * row;
             for (int j = 2; j < b.n_dims; ++j) {
                 uint64_t qq, rr;
                 divmod_dim(rem, dp[0], dp[1], qq, rr);
@@ -842,7 +845,7 @@ __device__ __forceinline__ void stream_store(const LoadedBucket &b, int64_t tid0
                                              const T (&acc)[V1 * V2], unsigned char *stage) {
     if constexpr ((BC == kBigInter2 || BC == kBigInter4) && V2 > 1) {
         if (tid < b.n_tiles) {
-            const int64_t os1 = b.dims[(int64_t)b.n_dims * (2 + b.n_in) + 1];
+            const int64_t os1 = as_const(b.dims)[(int64_t)b.n_dims * (2 + b.n_in) + 1];
             T *o = static_cast<T *>(b.out) + out_off;
 #pragma unroll
             for (int j2 = 0; j2 < V2; ++j2) store_n<T, V1, kNtStore, true>(o + j2 * os1, acc + j2 * V1);
