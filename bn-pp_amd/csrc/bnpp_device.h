@@ -37,7 +37,7 @@ constexpr int split_g_budget_bytes(int f, int eb = 4) {
            (eb == 8 && f == 8 ? (split_xch_bytes(f, eb) > split_img_bytes(f, eb) ? split_xch_bytes(f, eb) : split_img_bytes(f, eb))
                               : split_xch_bytes(f, eb) + split_img_bytes(f, eb));
 }
-constexpr int split_max_f(int eb) { return eb == 4 ? 8 : 8; }    // longest split run per element size
+constexpr int split_max_f(int) { return 8; }                    // longest split run (fp32 and fp64)
 constexpr int split_max_bel_f(int eb) { return eb == 4 ? 8 : 7; } // longest run forming a fused belief
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 
