@@ -126,8 +126,8 @@ constexpr int kStreamLdsBudget = 32768;    // bytes of LDS for the small inputs
 
 // Kernel variant: one instantiation per (input-count class, v1, v2) so every
 // launch gets the register allocation of its own shape (v1*8+v2 is unique over
-// the instantiated tiles 1x1 2x1 4x1 2x2 2x4 4x2 4x4 2x8).  So every
-// launch gets the register allocation of its own shape.
+// the instantiated tiles 1x1 2x1 4x1 2x2 2x4 4x2 4x4 2x8 and the whole-dim
+// rows 3x1 5x1 6x1 7x1).
 __host__ __device__ inline int nin_class(int n_in) { return n_in <= 1 ? 1 : n_in <= 2 ? 2 : n_in <= 4 ? 4 : 8; }
 __host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return nin_class(n_in) * 64 + v1 * 8 + v2; }
 // + kGenericO32: the same kernel with 32-bit table offsets, for launches whose
