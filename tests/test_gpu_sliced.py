@@ -141,3 +141,61 @@ def test_torch_collective_wraps_engine_buffers(ctx):
         assert (back == 7).all()
     finally:
         bnpp._lib.bnpp_free(ctx.handle, p)
+
+
+RCCL_WORKER = r"""
+import ctypes as C, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "bn-pp_amd", "python"))
+import numpy as np
+import torch
+import torch.distributed as dist
+import bnpp
+from bnpp import dist as bdist
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1)
+ctx = bnpp.Context(0)
+coll = bdist.TorchCollective(ctx, dist, 1, timeout_s=60)   # nccl groups + their first all-reduce
+assert coll.backend == "nccl" and len(coll.pool) == coll.LANES
+n = 1 << 20
+ptrs = []
+for _ in range(2):
+    p = C.c_void_p()
+    bnpp._check(bnpp._lib.bnpp_malloc(ctx.handle, n, C.byref(p)), "malloc")
+    ptrs.append(p.value)
+send, recv = ptrs
+src = (np.arange(n) * 7 % 253).astype(np.uint8)
+bnpp._check(bnpp._lib.bnpp_memcpy_h2d(ctx.handle, send, src.ctypes.data, n), "h2d")
+for op in (bnpp.COLL_ALLGATHER, bnpp.COLL_ALLTOALL):
+    zero = np.zeros(n, dtype=np.uint8)
+    bnpp._check(bnpp._lib.bnpp_memcpy_h2d(ctx.handle, recv, zero.ctypes.data, n), "h2d")
+    coll(op, send, recv, n, ctx.stream())              # RCCL on the engine's stream
+    ctx.synchronize()
+    back = np.empty(n, dtype=np.uint8)
+    bnpp._check(bnpp._lib.bnpp_memcpy_d2h(ctx.handle, back.ctypes.data, recv, n), "d2h")
+    assert np.array_equal(back, src), op
+assert coll.calls == 2 and len(coll.groups) == 1
+# bench.py's timer reduction over RCCL
+dist.barrier()
+tt = torch.tensor([3.5], device="cuda", dtype=torch.float64)
+dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+assert float(tt[0]) == 3.5
+for p in ptrs:
+    bnpp._check(bnpp._lib.bnpp_free(ctx.handle, p), "free")
+dist.destroy_process_group()
+ctx.close()
+print("rccl ok")
+"""
+
+
+def test_torch_collective_over_rccl_world1(tmp_path):
+    """The nccl (RCCL) branch of bnpp.dist.TorchCollective on the box's one GPU:
+    a one-rank nccl world creates the lanes' process groups, runs all-gather
+    and all-to-all on the engine's own stream over engine buffers, and the
+    bench's barrier + max-reduce -- the calls an 8-GPU run makes, minus the
+    peers (a one-GPU box cannot host two RCCL ranks)."""
+    script = tmp_path / "rccl_worker.py"
+    script.write_text(RCCL_WORKER)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    p = subprocess.run([sys.executable, str(script), REPO], env=env, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "rccl ok" in p.stdout
