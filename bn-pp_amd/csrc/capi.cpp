@@ -357,137 +357,189 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
         }
         const bool tt = std::getenv("BNPP_TIMING") != nullptr;
         double tq = now_ms();
-        plans.push_back(plan_bucket_tree(d.cards, views, ord, targets, part, n_parts));
         auto need = [&](const VEPlan &p) { return sat_add(plan_arena_bytes(p, eb), (int64_t)p.buckets.size() * 512); };
-        if (tt) std::fprintf(stderr, "[bnpp] bucket tree: tree plan %.1f ms\n", now_ms() - tq);
+        std::string msg;
         const char *force = std::getenv("BNPP_TREE_SLOTS");     // testing / tuning: chain mode, fixed slots
         if (force && std::atoi(force) > 0) {
-            std::string msg;
             VEPlan cp;
             if (!plan_bucket_tree_chain(d.cards, views, ord, targets, std::atoi(force), part, n_parts, cp, &msg, chain_eb,
                                         n_slices, slice_rank, false, eb))
                 return set_err(BNPP_ERR_UNSUPPORTED, msg);
-            plans.back() = std::move(cp);
-        } else if ((tq = now_ms(), need(plans.back()) > budget) || n_parts > 1 || n_slices > 1) {
-            if (tt) std::fprintf(stderr, "[bnpp] bucket tree: whole-tree need %.1f ms\n", now_ms() - tq);
-            // every forward message does not fit: recompute them from checkpoints
-            // (chain-shaped trees), with as many checkpoint slots as fit
-            std::string msg;
-            VEPlan best;
-            // sliced runs: the two-front schedule (two concurrent lanes, no
-            // recomputation) when its arena fits, else checkpointing on one lane
-            if (n_slices > 1 && !(tuning_knob("BNPP_SLICE_LANES") && *tuning_knob("BNPP_SLICE_LANES") == '0')) {
-                VEPlan cp;
-                if (plan_bucket_tree_chain(d.cards, views, ord, targets, 1, part, n_parts, cp, &msg, chain_eb, n_slices,
-                                           slice_rank, true, eb)) {
-                    if (need(cp) <= budget) {
-                        plans.back() = std::move(cp);
-                        return BNPP_OK;
-                    }
-                } else {
-                    return set_err(BNPP_ERR_UNSUPPORTED, msg);
+            plans.push_back(std::move(cp));
+            return BNPP_OK;
+        }
+        // plans the search leaves behind (the whole tree when it does not fit,
+        // unused probes: ~2 ms each to free) are freed off the call's path
+        std::vector<VEPlan> dead;
+        struct Burial {
+            std::vector<VEPlan> &d;
+            ~Burial() {
+                if (!d.empty()) std::thread([x = std::move(d)]() mutable { x.clear(); }).detach();
+            }
+        } burial{dead};
+        // when the forward messages do not all fit, they are recomputed from
+        // checkpoints (chain-shaped trees), with as many checkpoint slots as fit.
+        // The slot search needs only the order, so its memo's plan or its first
+        // probe round is planned beside the whole tree, which is used if it fits
+        int lo = 1, hi = n_slices > 1 ? 256 : 64, best_s = 0;
+        VEPlan best;
+        const uint64_t key = slot_key(d.cards, scopes, ord, targets, eb, chain_eb, part, n_parts, n_slices);
+        int memo_s = 0;
+        {
+            std::lock_guard<std::mutex> g(slot_memo().mu);
+            for (const SlotMemo::Entry &e : slot_memo().entries)
+                if (e.key == key && e.need_ok <= budget && budget < e.need_fail) memo_s = e.slots;
+        }
+        // first probe round: eight consecutive counts ending at the estimate
+        // budget / largest message (a checkpoint slot holds one message; the
+        // answer sits a few below it), so that one round usually brackets it
+        int first_hi = 0;
+        if (n_slices == 1 && memo_s == 0) {
+            const double est = (double)budget / (order_max_table(nv, d.cards, scopes, ord) * eb);
+            if (est >= 1 && est < hi) first_hi = (int)est;
+        }
+        std::vector<int> pre;                                // planned beside the whole tree
+        if (n_slices == 1 && memo_s > 0) {
+            pre.push_back(memo_s);
+        } else if (first_hi > 0) {
+            const int k = std::min(8, first_hi);             // first_hi - k + 1 .. first_hi (>= 1)
+            for (int i = 0; i < k; ++i) pre.push_back(first_hi - (k - 1) + i);
+            first_hi = 0;
+        }
+        const int npre = (int)pre.size();
+        std::vector<VEPlan> pre_cps(npre);
+        std::vector<int64_t> pre_nb(npre, 0);
+        std::vector<char> pre_ok(npre, 0);
+        std::vector<std::string> pre_msgs(npre);
+        VEPlan tree;
+        int64_t tree_need = 0;
+        parallel_for((int64_t)npre + 1, [&](int64_t i) {
+            if (i == 0) {
+                tree = plan_bucket_tree(d.cards, views, ord, targets, part, n_parts);
+                tree_need = need(tree);
+                return;
+            }
+            pre_ok[i - 1] = plan_bucket_tree_chain(d.cards, views, ord, targets, pre[i - 1], part, n_parts, pre_cps[i - 1],
+                                                   &pre_msgs[i - 1], chain_eb, n_slices, slice_rank, false, eb) ? 1 : 0;
+            if (pre_ok[i - 1]) pre_nb[i - 1] = need(pre_cps[i - 1]);
+        });
+        if (tt) std::fprintf(stderr, "[bnpp] bucket tree: whole tree beside %d checkpointed plans %.1f ms\n", npre, now_ms() - tq);
+        if (tree_need <= budget && n_parts == 1 && n_slices == 1) {
+            plans.push_back(std::move(tree));
+            for (VEPlan &c : pre_cps) dead.push_back(std::move(c));
+            return BNPP_OK;
+        }
+        dead.push_back(std::move(tree));
+        // sliced runs: the two-front schedule (two concurrent lanes, no
+        // recomputation) when its arena fits, else checkpointing on one lane
+        if (n_slices > 1 && !(tuning_knob("BNPP_SLICE_LANES") && *tuning_knob("BNPP_SLICE_LANES") == '0')) {
+            VEPlan cp;
+            if (plan_bucket_tree_chain(d.cards, views, ord, targets, 1, part, n_parts, cp, &msg, chain_eb, n_slices,
+                                       slice_rank, true, eb)) {
+                if (need(cp) <= budget) {
+                    plans.push_back(std::move(cp));
+                    return BNPP_OK;
                 }
+            } else {
+                return set_err(BNPP_ERR_UNSUPPORTED, msg);
             }
-            // sliced messages are 1/n_slices of the size: room for more checkpoints
-            int lo = 1, hi = n_slices > 1 ? 256 : 64, best_s = 0;
-            const uint64_t key = slot_key(d.cards, scopes, ord, targets, eb, chain_eb, part, n_parts, n_slices);
-            int memo_s = 0;
-            {
-                std::lock_guard<std::mutex> g(slot_memo().mu);
-                for (const SlotMemo::Entry &e : slot_memo().entries)
-                    if (e.key == key && e.need_ok <= budget && budget < e.need_fail) memo_s = e.slots;
-            }
-            if (memo_s > 0) {                             // the search would land on the same count
+        }
+        if (memo_s > 0) {                                    // the search would land on the same count
+            if (n_slices == 1) {
+                if (pre_ok[0] && pre_nb[0] <= budget) {
+                    best_s = memo_s;
+                    best = std::move(pre_cps[0]);
+                    lo = hi + 1;
+                }
+            } else {
                 VEPlan cp;
-                if (plan_bucket_tree_chain(d.cards, views, ord, targets, memo_s, part, n_parts, cp, &msg, chain_eb, n_slices,
-                                           slice_rank, false, eb) &&
+                if (plan_bucket_tree_chain(d.cards, views, ord, targets, memo_s, part, n_parts, cp, &msg, chain_eb,
+                                           n_slices, slice_rank, false, eb) &&
                     need(cp) <= budget) {
                     best_s = memo_s;
                     best = std::move(cp);
                     lo = hi + 1;
                 }
             }
-            int64_t need_ok = 0, need_fail = INT64_MAX;
-            bool exact = true;                            // every probe planned: the bracket is valid
-            // the need grows with the slot count: a k-ary search, up to 8
-            // probes planned in parallel per round (two rounds for 64 counts
-            // instead of six bisection steps; a cold call's planning time)
-            // first round: eight consecutive counts ending at the estimate
-            // budget / largest message (a checkpoint slot holds one message;
-            // the answer sits a few below it), so that one round usually
-            // brackets the answer and a second is not needed
-            int first_hi = 0;
-            if (lo <= hi && n_slices == 1) {
-                int64_t big = 1;
-                for (const MsgTable &t : plans.back().msgs) big = std::max(big, t.size);
-                const int64_t est = budget / sat_mul(big, eb);
-                if (est >= 1 && est < hi) first_hi = (int)est;
-            }
-            while (lo <= hi && exact) {
-                tq = now_ms();
-                const int m = hi - lo + 1;
-                int n = std::min(8, m);
-                std::vector<int> probe(n);                // ascending, inside [lo, hi]
-                for (int i = 0; i < n; ++i) probe[i] = m <= 8 ? lo + i : lo + (int)((int64_t)m * (i + 1) / (n + 1));
-                if (first_hi > 0 && m > 8) {
-                    const int k = std::min(n, first_hi);  // first_hi - k + 1 .. first_hi (>= 1)
-                    probe.resize(k);
-                    n = k;
-                    for (int i = 0; i < k; ++i) probe[i] = first_hi - (k - 1) + i;
-                    first_hi = 0;
+        }
+        int64_t need_ok = 0, need_fail = INT64_MAX;
+        bool exact = true;                                   // every probe planned: the bracket is valid
+        // one probe round's results (probes ascending): the need grows with the slot count
+        auto absorb = [&](const std::vector<int> &probe, std::vector<VEPlan> &cps, const std::vector<char> &planned,
+                          const std::vector<int64_t> &nb, const std::vector<std::string> &msgs) {
+            int new_lo = lo, new_hi = hi;
+            for (size_t i = 0; i < probe.size(); ++i) {
+                if (!planned[i]) {                           // as a bisection that stops at its first failure
+                    exact = false;
+                    if (msg.empty()) msg = msgs[i];
+                    new_hi = std::min(new_hi, probe[i] - 1);
+                    break;
                 }
-                std::vector<VEPlan> cps(n);
-                std::vector<int64_t> nb(n, 0);
-                std::vector<char> planned(n, 0);
-                std::vector<std::string> msgs(n);
-                std::vector<double> pt(n);
-                parallel_for((int64_t)n, [&](int64_t i) {
-                    const double a = now_ms();
-                    planned[i] = plan_bucket_tree_chain(d.cards, views, ord, targets, probe[i], part, n_parts, cps[i],
-                                                        &msgs[i], chain_eb, n_slices, slice_rank, false, eb) ? 1 : 0;
-                    if (planned[i]) nb[i] = need(cps[i]);
-                    pt[i] = now_ms() - a;
-                });
-                if (tt)
-                    for (int i = 0; i < n; ++i) std::fprintf(stderr, "[bnpp]   probe %d slots: %.1f ms\n", probe[i], pt[i]);
-                int new_lo = lo, new_hi = hi;
-                for (int i = 0; i < n; ++i) {
-                    if (!planned[i]) {                    // as a bisection that stops at its first failure
-                        exact = false;
-                        if (msg.empty()) msg = msgs[i];
-                        new_hi = std::min(new_hi, probe[i] - 1);
-                        break;
+                if (nb[i] <= budget) {
+                    if (probe[i] > best_s) {
+                        if (best_s > 0) dead.push_back(std::move(best));
+                        best_s = probe[i];
+                        best = std::move(cps[i]);
                     }
-                    if (nb[i] <= budget) {
-                        if (probe[i] > best_s) {
-                            best_s = probe[i];
-                            best = std::move(cps[i]);
-                        }
-                        need_ok = std::max(need_ok, nb[i]);   // valid for budgets >= every fitting probe's need
-                        new_lo = std::max(new_lo, probe[i] + 1);
-                    } else {
-                        need_fail = std::min(need_fail, nb[i]);
-                        new_hi = std::min(new_hi, probe[i] - 1);
-                        break;                            // larger probes need more still
-                    }
+                    need_ok = std::max(need_ok, nb[i]);      // valid for budgets >= every fitting probe's need
+                    new_lo = std::max(new_lo, probe[i] + 1);
+                } else {
+                    need_fail = std::min(need_fail, nb[i]);
+                    new_hi = std::min(new_hi, probe[i] - 1);
+                    break;                                   // larger probes need more still
                 }
-                lo = new_lo;
-                hi = new_hi;
-                if (tt) std::fprintf(stderr, "[bnpp] bucket tree: %d slot probes %.1f ms\n", n, now_ms() - tq);
             }
-            if (best_s > 0) {
-                if (best_s != memo_s && exact) {
-                    std::lock_guard<std::mutex> g(slot_memo().mu);
-                    auto &en = slot_memo().entries;
-                    if (en.size() >= 64) en.erase(en.begin());
-                    en.push_back({key, best_s, need_ok, need_fail});
-                }
-                if (std::getenv("BNPP_TIMING")) std::fprintf(stderr, "[bnpp] bucket tree: %d checkpoint slots\n", best_s);
-                plans.back() = std::move(best);
-            } else if (n_slices > 1) {
-                return set_err(msg.empty() ? BNPP_ERR_OOM : BNPP_ERR_UNSUPPORTED,
-                               msg.empty() ? "sliced bucket tree: no checkpoint count fits the memory budget" : msg);
+            lo = new_lo;
+            hi = new_hi;
+            for (VEPlan &c : cps) dead.push_back(std::move(c));
+        };
+        if (lo <= hi && memo_s == 0 && npre > 0) absorb(pre, pre_cps, pre_ok, pre_nb, pre_msgs);
+        else
+            for (VEPlan &c : pre_cps) dead.push_back(std::move(c));
+        // further rounds: a k-ary search, up to 8 probes planned in parallel per
+        // round (two rounds for 64 counts instead of six bisection steps)
+        while (lo <= hi && exact) {
+            tq = now_ms();
+            const int m = hi - lo + 1;
+            int n = std::min(8, m);
+            std::vector<int> probe(n);                       // ascending, inside [lo, hi]
+            for (int i = 0; i < n; ++i) probe[i] = m <= 8 ? lo + i : lo + (int)((int64_t)m * (i + 1) / (n + 1));
+            if (first_hi > 0 && m > 8) {                     // (a memo plan that no longer fit)
+                const int k = std::min(n, first_hi);
+                probe.resize(k);
+                n = k;
+                for (int i = 0; i < k; ++i) probe[i] = first_hi - (k - 1) + i;
+                first_hi = 0;
             }
+            std::vector<VEPlan> cps(n);
+            std::vector<int64_t> nb(n, 0);
+            std::vector<char> planned(n, 0);
+            std::vector<std::string> msgs(n);
+            parallel_for((int64_t)n, [&](int64_t i) {
+                planned[i] = plan_bucket_tree_chain(d.cards, views, ord, targets, probe[i], part, n_parts, cps[i],
+                                                    &msgs[i], chain_eb, n_slices, slice_rank, false, eb) ? 1 : 0;
+                if (planned[i]) nb[i] = need(cps[i]);
+            });
+            absorb(probe, cps, planned, nb, msgs);
+            if (tt) std::fprintf(stderr, "[bnpp] bucket tree: %d slot probes %.1f ms\n", n, now_ms() - tq);
+        }
+        if (best_s > 0) {
+            if (best_s != memo_s && exact) {
+                std::lock_guard<std::mutex> g(slot_memo().mu);
+                auto &en = slot_memo().entries;
+                if (en.size() >= 64) en.erase(en.begin());
+                en.push_back({key, best_s, need_ok, need_fail});
+            }
+            if (tt) std::fprintf(stderr, "[bnpp] bucket tree: %d checkpoint slots\n", best_s);
+            plans.push_back(std::move(best));
+        } else if (n_slices > 1) {
+            return set_err(msg.empty() ? BNPP_ERR_OOM : BNPP_ERR_UNSUPPORTED,
+                           msg.empty() ? "sliced bucket tree: no checkpoint count fits the memory budget" : msg);
+        } else {
+            // no checkpoint count fits (or the tree is not a chain): the whole
+            // tree, which plan_schedules reports as over the budget
+            plans.push_back(std::move(dead.front()));
+            dead.erase(dead.begin());
         }
     } else {
         // one independent VE per target (model.cpp:326-334), planned in parallel

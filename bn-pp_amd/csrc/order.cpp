@@ -187,4 +187,29 @@ int order_width(int n, const std::vector<std::vector<int>> &scopes, const std::v
     return width;
 }
 
+// entries of the largest table `order` makes (the product of the cards of a
+// variable's neighbours when it is eliminated: its bucket's message)
+double order_max_table(int n, const std::vector<int> &cards, const std::vector<std::vector<int>> &scopes,
+                       const std::vector<int> &order) {
+    BitGraph g = build(n, scopes);
+    std::vector<int> nb;
+    double big = 1;
+    for (int v : order) {
+        g.neighbours(v, nb);
+        double t = 1;
+        for (int a : nb) t *= cards[a];
+        big = std::max(big, t);
+        for (int a : nb) g.clr(a, v);
+        for (size_t i = 0; i < nb.size(); ++i)
+            for (size_t j = 0; j < nb.size(); ++j)
+                if (i != j) g.set(nb[i], nb[j]);
+        if (g.present[v]) {
+            std::fill(g.row(v), g.row(v) + g.words, 0);
+            g.present[v] = 0;
+            g.n_present--;
+        }
+    }
+    return big;
+}
+
 }  // namespace bnpp

@@ -18,4 +18,9 @@ int elimination_order(int n_model_vars, const std::vector<int> &cards, const std
 // Graph::order_width (graph.cpp:197-237)
 int order_width(int n_model_vars, const std::vector<std::vector<int>> &scopes, const std::vector<int> &order);
 
+// entries of the largest message eliminating in `order` makes (a symbolic pass:
+// the checkpoint-slot search's first estimate, before any plan exists)
+double order_max_table(int n_model_vars, const std::vector<int> &cards, const std::vector<std::vector<int>> &scopes,
+                       const std::vector<int> &order);
+
 }  // namespace bnpp

@@ -5,7 +5,7 @@
 # self-launched two-rank rehearsal.
 set -o pipefail
 R=$PWD
-OUT=$R/gpurun_out/final5d
+OUT=$R/gpurun_out/final5f
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
