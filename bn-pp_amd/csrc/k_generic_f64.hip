@@ -1,14 +1,19 @@
 // Kernel instantiations compiled as a separate translation unit (parallel build).
+// Generic gather kernels, tiles along one output dim; two-dim tiles are in
+// k_generic2_f64.hip.
 #include "kernels.cuh"
 
 namespace bnpp {
 
+hipError_t dispatch_level_f64_2d(int key, const LevelArgs &a, int max_grid, hipStream_t stream);
+hipError_t dispatch_single_f64_2d(int key, const SingleArgs &a, int max_grid, hipStream_t stream);
+
 hipError_t dispatch_level_f64(int key, const LevelArgs &a, int max_grid, hipStream_t stream) {
-    switch (key) { BNPP_ALL(BNPP_CASE_LEVEL, BNPP_TILES_F64, double) default: break; }
-    return hipErrorInvalidValue;
+    switch (key) { BNPP_ALL(BNPP_CASE_LEVEL, BNPP_TILES_1D, double) default: break; }
+    return dispatch_level_f64_2d(key, a, max_grid, stream);
 }
 hipError_t dispatch_single_f64(int key, const SingleArgs &a, int max_grid, hipStream_t stream) {
-    switch (key) { BNPP_ALL(BNPP_CASE_SINGLE, BNPP_TILES_F64, double) default: break; }
-    return hipErrorInvalidValue;
+    switch (key) { BNPP_ALL(BNPP_CASE_SINGLE, BNPP_TILES_1D, double) default: break; }
+    return dispatch_single_f64_2d(key, a, max_grid, stream);
 }
 }  // namespace bnpp

@@ -1025,10 +1025,11 @@ static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_
 
 // (3, 1) (5, 1) (6, 1) (7, 1): a whole fastest dim of that card per thread
 #define BNPP_TILES_ODD(X, T, NIN) X(T, NIN, 3, 1) X(T, NIN, 5, 1) X(T, NIN, 6, 1) X(T, NIN, 7, 1)
-#define BNPP_TILES_F32(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
-    X(T, NIN, 4, 2) X(T, NIN, 4, 4) X(T, NIN, 2, 8) BNPP_TILES_ODD(X, T, NIN)
-#define BNPP_TILES_F64(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) X(T, NIN, 2, 2) X(T, NIN, 2, 4) \
-    X(T, NIN, 4, 2) BNPP_TILES_ODD(X, T, NIN)
+// tiles along one output dim (k_generic_*.hip) and along two (k_generic2_*.hip,
+// compiled without SimplifyCFG's store sinking: Makefile)
+#define BNPP_TILES_1D(X, T, NIN) X(T, NIN, 1, 1) X(T, NIN, 2, 1) X(T, NIN, 4, 1) BNPP_TILES_ODD(X, T, NIN)
+#define BNPP_TILES_F32_2D(X, T, NIN) X(T, NIN, 2, 2) X(T, NIN, 2, 4) X(T, NIN, 4, 2) X(T, NIN, 4, 4) X(T, NIN, 2, 8)
+#define BNPP_TILES_F64_2D(X, T, NIN) X(T, NIN, 2, 2) X(T, NIN, 2, 4) X(T, NIN, 4, 2)
 #define BNPP_ALL(X, TILES, T) TILES(X, T, 1) TILES(X, T, 2) TILES(X, T, 4) TILES(X, T, 8)
 
 #define BNPP_CASE_LEVEL(T, NIN, V1, V2) \
