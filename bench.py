@@ -22,9 +22,11 @@ single core, on a bounded sample of the same bucket shape.
 "mar": the metric's second half on its own instance -- all marginals of the
 32x32 Ising grid UAI (BASELINE config 3) through the checkpointed two-pass
 bucket tree (column-sweep order, width 32, fp32), split over the ranks by
-chain segments; wall-clock like the reference's uptime, warm (second call on
-the context, arena reused; "cold_wall_ms" = the first call), each with its
-phase split (bnpp_last_timing).  It runs after the bucket and the CPU
+chain segments; wall-clock like the reference's uptime, warm (the identical
+second call on the context: the cached job relaunched -- no ordering or
+planning -- in its arena; "cold_wall_ms" = the first call, which orders,
+plans, allocates the arena and loads the kernels), each with its phase split
+(bnpp_last_timing).  It runs after the bucket and the CPU
 baseline: HBM freed by an earlier process is cleared by the driver in the
 background for several seconds, and a first touch before that waits for it
 (profiles/r03_cold_after_free.jsonl).  "check": P(x_t = 0) of three targets

@@ -51,6 +51,7 @@ struct bnpp_ctx {
     // and planning.  Guarded by cache_mu, like the arena it runs in
     bnpp_job *job_cached = nullptr;
     uint64_t job_key = 0;
+    int64_t job_budget = 0;             // the memory budget the cached job was planned under
 };
 // live contexts: bnpp_model_free releases what they cache for the model
 std::mutex g_ctxs_mu;
@@ -834,8 +835,7 @@ void evict_cached_job(bnpp_ctx *ctx) {
 
 // key of a one-shot call for the job cache (0: do not cache)
 uint64_t call_key(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, const int *ev_vals, int heuristic,
-                  const int *order, int n_order, int n_targets, const int *targets, int dtype, int part, int n_parts,
-                  int64_t budget) {
+                  const int *order, int n_order, int n_targets, const int *targets, int dtype, int part, int n_parts) {
     if (std::getenv("BNPP_NO_JOB_CACHE")) return 0;
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
@@ -855,7 +855,6 @@ uint64_t call_key(const bnpp_model *m, int kind, int n_ev, const int *ev_vars, c
     mix((uint64_t)dtype);
     mix((uint64_t)part);
     mix((uint64_t)n_parts);
-    mix((uint64_t)(budget >> 30));                       // the plan depends on the budget (GiB)
     mix_plan_knobs(mix);
     return h ? h : 1;
 }
@@ -949,13 +948,24 @@ int job_results_sliced(bnpp_job *job, hipStream_t stream, double *out, int64_t *
     return BNPP_OK;
 }
 
+// The plan depends on the memory budget (free memory, the cached arena
+// counted as free), which moves a little between identical calls as other
+// allocations come and go: within 2 % of the budget the cached job was
+// planned under it is relaunched (its arena is allocated already, and a
+// checkpoint count planned for a slightly different budget gives the same
+// results); beyond that the call plans afresh
+bool same_budget(int64_t a, int64_t b) {
+    const int64_t d = a > b ? a - b : b - a;
+    return a > 0 && b > 0 && d * 50 <= (a > b ? a : b);
+}
+
 // A one-shot call's job: the context's cached one when the call is identical
 // (its planning phases read 0), else a new one (create).  cache_ok: the call
 // holds cache_mu (it runs in the cached arena)
 template <typename Create>
-int oneshot_job(bnpp_ctx *ctx, bool cache_ok, uint64_t key, Create &&create, bnpp_job *&job) {
+int oneshot_job(bnpp_ctx *ctx, bool cache_ok, uint64_t key, int64_t budget, Create &&create, bnpp_job *&job) {
     job = nullptr;
-    if (cache_ok && key && ctx->job_cached && ctx->job_key == key) {
+    if (cache_ok && key && ctx->job_cached && ctx->job_key == key && same_budget(ctx->job_budget, budget)) {
         job = ctx->job_cached;
         ctx->job_cached = nullptr;
         ctx->job_key = 0;
@@ -971,12 +981,13 @@ int oneshot_job(bnpp_ctx *ctx, bool cache_ok, uint64_t key, Create &&create, bnp
 }
 
 // after the call: keep a good job for the next identical call, free the rest
-void oneshot_done(bnpp_ctx *ctx, bool cache_ok, uint64_t key, bnpp_job *job, int rc) {
+void oneshot_done(bnpp_ctx *ctx, bool cache_ok, uint64_t key, int64_t budget, bnpp_job *job, int rc) {
     if (!job) return;
     if (rc == BNPP_OK && cache_ok && key) {
         evict_cached_job(ctx);
         ctx->job_cached = job;
         ctx->job_key = key;
+        ctx->job_budget = budget;
     } else {
         destroy_job(job);
     }
@@ -1506,9 +1517,10 @@ int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     bnpp_job *job = nullptr;
     std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
     const bool cache_ok = lk.owns_lock();
+    const int64_t budget = memory_budget(ctx, true);
     const uint64_t key = cache_ok ? call_key(m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype,
-                                             0, 1, memory_budget(ctx, true)) : 0;
-    int rc = oneshot_job(ctx, cache_ok, key, [&](std::unique_ptr<bnpp_job> &j) {
+                                             0, 1) : 0;
+    int rc = oneshot_job(ctx, cache_ok, key, budget, [&](std::unique_ptr<bnpp_job> &j) {
         return create_job(ctx, m, 0, n_ev, ev_vars, ev_vals, heuristic, order, n_order, 0, nullptr, dtype, j, 0, 1,
                           cache_ok);
     }, job);
@@ -1518,7 +1530,7 @@ int bnpp_partition(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     double lz = 0, zz = 0;
     if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, &lz, &zz);
     const double t3 = now_ms();
-    oneshot_done(ctx, cache_ok, key, job, rc);
+    oneshot_done(ctx, cache_ok, key, budget, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (rc) return rc;
     if (log10_z) *log10_z = lz;
@@ -1537,9 +1549,10 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     bnpp_job *job = nullptr;
     std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
     const bool cache_ok = lk.owns_lock();
+    const int64_t budget = memory_budget(ctx, true);
     const uint64_t key = cache_ok ? call_key(m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets,
-                                             dtype, 0, 1, memory_budget(ctx, true)) : 0;
-    int rc = oneshot_job(ctx, cache_ok, key, [&](std::unique_ptr<bnpp_job> &j) {
+                                             dtype, 0, 1) : 0;
+    int rc = oneshot_job(ctx, cache_ok, key, budget, [&](std::unique_ptr<bnpp_job> &j) {
         return create_job(ctx, m, 1, n_ev, ev_vars, ev_vals, heuristic, nullptr, 0, n_targets, targets, dtype, j, 0, 1,
                           cache_ok);
     }, job);
@@ -1548,7 +1561,7 @@ int bnpp_marginals(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const int *ev_v
     const double t2 = now_ms();
     if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, out, nullptr);
     const double t3 = now_ms();
-    oneshot_done(ctx, cache_ok, key, job, rc);
+    oneshot_done(ctx, cache_ok, key, budget, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (std::getenv("BNPP_TIMING"))
         std::fprintf(stderr, "[bnpp] marginals: create %.1f ms, launch %.1f ms, run+fetch %.1f ms, free %.1f ms\n",
@@ -1577,9 +1590,10 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
     bnpp_job *job = nullptr;
     std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
     const bool cache_ok = lk.owns_lock();
+    const int64_t budget = memory_budget(ctx, true);
     const uint64_t key = cache_ok ? call_key(m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets,
-                                             targets, dtype, part, n_parts, memory_budget(ctx, true)) : 0;
-    int rc = oneshot_job(ctx, cache_ok, key, [&](std::unique_ptr<bnpp_job> &j) {
+                                             targets, dtype, part, n_parts) : 0;
+    int rc = oneshot_job(ctx, cache_ok, key, budget, [&](std::unique_ptr<bnpp_job> &j) {
         return create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, j,
                           part, n_parts, cache_ok);
     }, job);
@@ -1588,7 +1602,7 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
     const double t2 = now_ms();
     if (rc == BNPP_OK) rc = job_results(job, ctx->c.stream, out, nullptr, owned);
     const double t3 = now_ms();
-    oneshot_done(ctx, cache_ok, key, job, rc);
+    oneshot_done(ctx, cache_ok, key, budget, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (timing)
         std::fprintf(stderr, "[bnpp] tree marginals: create %.1f ms, launch %.1f ms, run+fetch %.1f ms, free %.1f ms\n",
