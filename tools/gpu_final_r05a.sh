@@ -4,7 +4,7 @@
 # WRITE_SIZE in separate --pmc passes, fp32 and fp64).
 set -o pipefail
 R=$PWD
-OUT=$R/gpurun_out/final5e
+OUT=$R/gpurun_out/final5i
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }

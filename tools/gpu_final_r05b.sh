@@ -5,7 +5,7 @@
 # self-launched two-rank rehearsal.
 set -o pipefail
 R=$PWD
-OUT=$R/gpurun_out/final5f
+OUT=$R/gpurun_out/final5h
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
