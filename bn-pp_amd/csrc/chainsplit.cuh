@@ -298,11 +298,19 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 #ifndef BNPP_F64_ALIAS
 #define BNPP_F64_ALIAS 1
 #endif
+// BNPP_F64_BEL_ALIAS=1 (variant builds): fp64 runs forming a fused belief on
+// the aliased layout too (two 8-wave workgroups per CU at 128 VGPRs, 76 B
+// spilled): 29.0 -> 31.9 ms per run of 7, fp64 32x32 MAR 8.21 -> 8.31 s,
+// results bit-identical (profiles/r05_f64_belief_alias_ab.txt); off
+#ifndef BNPP_F64_BEL_ALIAS
+#define BNPP_F64_BEL_ALIAS 0
+#endif
 // (fp64 runs of 8 need it in every kernel they have: one-run and multi-run;
 // they form no fused belief, so there is no MODE 1 kernel of them)
 template <typename T, int MODE, int F>
 __host__ __device__ constexpr bool split_alias() {
-    return sizeof(T) == 8 && (((BNPP_F64_ALIAS != 0 || F == 8) && MODE == 0) || (F == 8 && MODE == 2));
+    return sizeof(T) == 8 && (((BNPP_F64_ALIAS != 0 || F == 8) && MODE == 0) || (F == 8 && MODE == 2) ||
+                              (BNPP_F64_BEL_ALIAS != 0 && MODE == 1));
 }
 template <int F, int EB, bool ALIAS>
 __host__ __device__ constexpr int split_tile_lds() {

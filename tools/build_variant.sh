@@ -12,7 +12,9 @@ rm -f build_$name/*.o
 pids=()
 for src in csrc/*.hip; do
   f=$(basename $src .hip)
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Icsrc -I../include $flags \
+  extra=""
+  case $f in k_generic2_*) extra="-mllvm -sink-common-insts=false";; esac     # as the Makefile
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Icsrc -I../include $flags $extra \
       -c $src -o build_$name/$f.o &
   pids+=($!)
 done
