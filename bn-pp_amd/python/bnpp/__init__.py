@@ -21,10 +21,15 @@ if not os.path.exists(LIB_PATH):
 # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.  When it
 # is installed, load it first so libbnpp binds to that same runtime (with two
 # runtimes in one process, whichever initialises second sees no device).
-try:
-    import torch  # noqa: F401
-except ImportError:
-    pass
+# BNPP_NO_TORCH=1 leaves PyTorch out of a process that does not use it: libbnpp
+# then binds to ROCm's runtime.  That is also the way to run under
+# HIP_ENABLE_DEFERRED_LOADING=0, where `import torch` itself segfaults on this
+# image (PyTorch 2.10+rocm7.0, inside `from torch._C import *`).
+if os.environ.get("BNPP_NO_TORCH") != "1":
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 _lib = C.CDLL(LIB_PATH)
 
 OK, ERR_INVALID, ERR_NO_DEVICE, ERR_OOM, ERR_HIP, ERR_IO, ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
