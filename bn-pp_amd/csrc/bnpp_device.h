@@ -105,6 +105,10 @@ struct BucketDesc {
     int64_t outer_div[2];
     // slab level launches: passes of kBlock / lanes tiles per block (0/1, or 2)
     int32_t slab_r;
+    // slab form whose tile row (C0 = v1 entries) spans output dims 0 and 1:
+    // the card of dim 0 (the small inputs' y offset is (y % slab_y2) * stride0
+    // + (y / slab_y2) * stride1); 0 when the row is output dim 0 alone
+    int32_t slab_y2;
 };
 constexpr int kSlabMaxOuter = 64;
 
@@ -134,12 +138,19 @@ __host__ __device__ inline int variant_key(int n_in, int v1, int v2) { return ni
 // every input is under 4 GiB (generic_o32)
 constexpr int kGenericO32 = 1024;
 __host__ __device__ inline bool generic_o32(int64_t max_in_bytes) { return max_in_bytes <= (int64_t)0xffffffff; }
-// stream kernels: 4096 + big-class * 256 + v1 * 16 + v2  (v1, v2 <= 8)
-__host__ __device__ inline int stream_key(int bcls, int v1, int v2) { return 4096 + bcls * 256 + v1 * 16 + v2; }
+// stream kernels: 4096 + big-class * 256 + v1 * 16 + v2  (v1, v2 <= 8), + kStream8In
+// for buckets of 5-8 inputs (their own instantiations: kernels.cuh NI = 8)
+constexpr int kStream8In = 2048;
+constexpr int kStream8Bcls = 5;            // big classes Row .. One (no interleaved forms) for 5-8 inputs
+__host__ __device__ inline int stream_key(int bcls, int v1, int v2, int n_in = 0) {
+    return 4096 + (n_in > 4 ? kStream8In : 0) + bcls * 256 + v1 * 16 + v2;
+}
 // slab kernels (slab.cuh): K summed values, C0 entries of output dim 0, V slow-dim entries per lane
 // and R passes of tiles per block (level launches, BucketDesc::slab_r: 1 or 2)
-__host__ __device__ constexpr int slab_key(int k, int c0, int v, int h = 1, int r = 1) {
-    return 16384 + k * 1024 + (r == 4 ? 512 : r == 2 ? 256 : 0) + c0 * 16 + v + (h == 2 ? 8 : 0);
+// + kSlab8In for buckets of 5-8 inputs (their own instantiations: slab.cuh NI = 8)
+constexpr int kSlab8In = 8192;
+__host__ __device__ constexpr int slab_key(int k, int c0, int v, int h = 1, int r = 1, int n_in = 0) {
+    return 16384 + (n_in > 4 ? kSlab8In : 0) + k * 1024 + (r == 4 ? 512 : r == 2 ? 256 : 0) + c0 * 16 + v + (h == 2 ? 8 : 0);
 }
 
 // Chain (sweep) form: F consecutive buckets of an elimination chain in one

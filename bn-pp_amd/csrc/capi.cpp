@@ -142,11 +142,7 @@ int run_single(bnpp_ctx *ctx, void *stream, int dtype, const std::vector<int> &c
     for (size_t i = 0; i < in_ptrs.size(); ++i) {
         a.meta[i].ptr = const_cast<void *>(in_ptrs[i]);
         // entries the view can reach (the launcher picks 32-bit offsets by it)
-        const View &v = b.in[i];
-        int64_t span = v.base + 1;
-        for (size_t j = 0; j < v.vars.size() && j < v.strides.size(); ++j)
-            span += sat_mul(cards[v.vars[j]] - 1, v.strides[j]);
-        a.meta[i].size = span;
+        a.meta[i].size = view_span(b.in[i], cards);
     }
     // BNPP_NO_O32=1 (tests): claim a span that rules out the 32-bit-offset kernels
     if (const char *no32 = std::getenv("BNPP_NO_O32"); no32 && *no32 == '1')
@@ -451,6 +447,12 @@ int build_plans(const ModelData &d, const std::vector<int> &ev, int kind, int he
                     best_s = memo_s;
                     best = std::move(pre_cps[0]);
                     lo = hi + 1;
+                } else {
+                    // the memo's count no longer fits this budget: search below
+                    // it, the first round ending at the budget's estimate
+                    if (pre_ok[0]) hi = std::min(hi, memo_s - 1);
+                    const double est = (double)budget / (order_max_table(nv, d.cards, scopes, ord) * eb);
+                    if (est >= 1 && est < hi) first_hi = (int)est;
                 }
             } else {
                 VEPlan cp;
@@ -1318,16 +1320,31 @@ int bnpp_model_free(bnpp_model *m) {
     // every live context drops the model's uploaded sources and a cached
     // one-shot job planned for it (a context in the middle of a call keeps
     // its job until its next one-shot call replaces it)
-    std::lock_guard<std::mutex> g(g_ctxs_mu);
-    for (bnpp_ctx *ctx : g_ctxs) {
-        {
-            std::lock_guard<std::mutex> gs(ctx->src_mu);
-            ctx->srcs.erase(std::remove_if(ctx->srcs.begin(), ctx->srcs.end(),
-                                           [&](const bnpp_ctx::Src &e) { return e.uid == m->uid; }),
-                            ctx->srcs.end());
+    // The contexts holding such a job are collected under the context list's
+    // lock; their jobs are destroyed after it is released (destroy_job waits
+    // for the device: other threads' ctx_create / ctx_destroy / model_free do
+    // not wait with it), each under its own context's cache lock, and the
+    // caller's current device is restored afterwards.
+    std::vector<std::pair<bnpp_ctx *, std::unique_lock<std::mutex>>> evict;
+    {
+        std::lock_guard<std::mutex> g(g_ctxs_mu);
+        for (bnpp_ctx *ctx : g_ctxs) {
+            {
+                std::lock_guard<std::mutex> gs(ctx->src_mu);
+                ctx->srcs.erase(std::remove_if(ctx->srcs.begin(), ctx->srcs.end(),
+                                               [&](const bnpp_ctx::Src &e) { return e.uid == m->uid; }),
+                                ctx->srcs.end());
+            }
+            std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
+            if (lk.owns_lock() && ctx->job_cached && ctx->job_cached->model_uid == m->uid)
+                evict.emplace_back(ctx, std::move(lk));
         }
-        std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
-        if (lk.owns_lock() && ctx->job_cached && ctx->job_cached->model_uid == m->uid) evict_cached_job(ctx);
+    }
+    if (!evict.empty()) {
+        int dev = -1;
+        const bool had = hipGetDevice(&dev) == hipSuccess;
+        for (auto &e : evict) evict_cached_job(e.first);
+        if (had) (void)hipSetDevice(dev);
     }
     delete m;
     return BNPP_OK;

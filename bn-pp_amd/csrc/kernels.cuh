@@ -637,7 +637,11 @@ struct BigTile {
     }
 };
 
-constexpr int kStreamMaxIn = 4;     // stream form: at most 4 inputs (planner-enforced)
+constexpr int kStreamMaxIn = 4;     // stream form: inputs of the default class (planner-enforced)
+// a stream bucket of 5-8 inputs (one big, the rest small) launches its own
+// instantiation, NI = 8 (stream_key(..., n_in)): the conditioned 32x32 PR's
+// 5-input bucket over an 8-GiB message ran 46 ms on the generic 8-input kernel
+// with 64-bit offsets
 
 struct StreamState {
     int big;
@@ -648,15 +652,15 @@ struct StreamState {
 // NTL: nontemporal loads of the big input -- the single-op calls (cold, user
 // tables: measured -2 % on the bench bucket); level kernels keep kNtLoad (a
 // VE chain re-reads the message the previous bucket just wrote)
-template <typename T, int V1, int V2, int BC, bool NTL>
+template <typename T, int V1, int V2, int BC, bool NTL, int NI = kStreamMaxIn>
 __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const StreamState &st, const T *small,
                                                  int64_t tid, T (&acc)[V1 * V2], int64_t &out_off) {
     constexpr bool kRows = (BC == kBigInter2 || BC == kBigInter4) && V2 > 1;   // output rows at a stride
     constexpr int TS = V1 * V2;
     using BT = BigTile<T, V1, V2, BC>;
-    int64_t pos[kStreamMaxIn];
+    int64_t pos[NI];
 #pragma unroll
-    for (int i = 0; i < kStreamMaxIn; ++i) pos[i] = b.base[i];
+    for (int i = 0; i < NI; ++i) pos[i] = b.base[i];
     out_off = 0;
     if (b.n_dims > 0) {
         const int row = 2 + b.n_in;
@@ -668,14 +672,14 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
         divmod_dim((uint64_t)tid, b.t0h, b.t0m, q, r);
         int64_t i0 = (int64_t)r * V1;
 #pragma unroll
-        for (int i = 0; i < kStreamMaxIn; ++i) pos[i] += i0 * b.s0[i];
+        for (int i = 0; i < NI; ++i) pos[i] += i0 * b.s0[i];
         if constexpr (kRows) out_off = i0 * os[0];
         if (b.n_dims > 1) {
             uint64_t q1, r1;
             divmod_dim(q, b.t1h, b.t1m, q1, r1);
             int64_t i1 = (int64_t)r1 * V2;
 #pragma unroll
-            for (int i = 0; i < kStreamMaxIn; ++i) pos[i] += i1 * b.s1[i];
+            for (int i = 0; i < NI; ++i) pos[i] += i1 * b.s1[i];
             if constexpr (kRows) out_off += i1 * os[1];
             uint64_t rem = q1;
             cst_t<int64_t> *dp = as_const(b.dims) + 2 * row;
@@ -683,7 +687,7 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
                 uint64_t qq, rr;
                 divmod_dim(rem, dp[0], dp[1], qq, rr);
 #pragma unroll
-                for (int i = 0; i < kStreamMaxIn; ++i)
+                for (int i = 0; i < NI; ++i)
                     if (i < b.n_in) pos[i] += (int64_t)rr * dp[2 + i];
                 if constexpr (kRows) out_off += (int64_t)rr * os[j];
                 rem = qq;
@@ -693,11 +697,11 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
     }
     // LDS-relative positions of the small inputs; the big input's address and
     // strides picked with static indices (a runtime index would go to scratch)
-    int32_t rel[kStreamMaxIn];
+    int32_t rel[NI];
     const T *bsrc = nullptr;
     int64_t bes = 0, bs0 = 0, bs1 = 0;
 #pragma unroll
-    for (int i = 0; i < kStreamMaxIn; ++i) {
+    for (int i = 0; i < NI; ++i) {
         rel[i] = st.lds_off[i] + (int32_t)(pos[i] - b.base[i]);
         if (i == st.big) {
             bsrc = static_cast<const T *>(b.ptr[i]) + pos[i];
@@ -711,7 +715,7 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
     // big one (interleaved path; the streamed path below keeps it inline)
     auto smalls = [&](int v, T (&p)[TS], auto &&big_apply) {
 #pragma unroll
-        for (int i = 0; i < kStreamMaxIn; ++i) {
+        for (int i = 0; i < NI; ++i) {
             if (i >= b.n_in) break;                         // uniform
             if (i == st.big) {
                 big_apply(p);
@@ -790,7 +794,7 @@ __device__ __forceinline__ T compute_stream_tile(const LoadedBucket &b, const St
 #pragma unroll
                 for (int j = 0; j < TS; ++j) p[j] = T(1);
 #pragma unroll
-                for (int i = 0; i < kStreamMaxIn; ++i) {
+                for (int i = 0; i < NI; ++i) {
                     if (i >= b.n_in) break;                         // uniform
                     if (i == st.big) {
                         BT::apply(bb[u], p);
@@ -857,11 +861,11 @@ __device__ __forceinline__ void stream_store(const LoadedBucket &b, int64_t tid0
 }
 
 // copy every small input of the bucket into LDS (uniform control flow)
-template <typename T>
+template <typename T, int NI = kStreamMaxIn>
 __device__ __forceinline__ void stage_small(const LoadedBucket &b, const StreamState &st, T *small) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kStreamMaxIn; ++i) {            // static indices: no scratch
+    for (int i = 0; i < NI; ++i) {                      // static indices: no scratch
         if (i >= b.n_in) break;
         if (i == st.big) continue;
         const T *src = static_cast<const T *>(b.ptr[i]) + b.base[i];
@@ -883,7 +887,7 @@ constexpr int kRedBytes = 64;       // block max reduction scratch at the head o
 #ifndef BNPP_STREAM_MINWAVES
 #define BNPP_STREAM_MINWAVES 1
 #endif
-template <typename T, int V1, int V2, int BC>
+template <typename T, int V1, int V2, int BC, int NI>
 __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                               const int64_t *__restrict__ pool,
                                                               TableMeta *__restrict__ meta, int64_t total_vblocks) {
@@ -926,14 +930,14 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_level_ker
             }
             b.neg_e = (int)(-e_sum);
             if (vb == cur_begin && threadIdx.x == 0) meta[d.out_table].exp2 = x_sum;
-            stage_small<T>(b, st, small);
+            stage_small<T, NI>(b, st, small);
         }
         const int64_t tid0 = (vb - cur_begin) * kBlock;
         const int64_t tid = tid0 + threadIdx.x;
         T acc[V1 * V2];
         int64_t oo = 0;
         if (tid < b.n_tiles) {
-            T m = compute_stream_tile<T, V1, V2, BC, kNtLoad>(b, st, small, tid, acc, oo);
+            T m = compute_stream_tile<T, V1, V2, BC, kNtLoad, NI>(b, st, small, tid, acc, oo);
             lmax = m > lmax ? m : lmax;
         }
         stream_store<T, V1, V2, BC>(b, tid0, tid, oo, acc, stage);
@@ -941,7 +945,7 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_level_ker
     if (cur >= 0) flush_max<T>(lmax, meta, descs[cur].out_table, descs[cur].flags, red);
 }
 
-template <typename T, int V1, int V2, int BC>
+template <typename T, int V1, int V2, int BC, int NI>
 __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_single_kernel(const SingleArgs args) {
 #if defined(__HIP_DEVICE_COMPILE__)
     (void)args;
@@ -961,14 +965,14 @@ __global__ __launch_bounds__(kBlock, BNPP_STREAM_MINWAVES) void stream_single_ke
     b.neg_e = 0;
     b.out = a.meta[d.n_in].ptr;
     for (int i = 0; i < kMaxIn; ++i) b.ptr[i] = i < d.n_in ? a.meta[i].ptr : nullptr;
-    stage_small<T>(b, st, small);
+    stage_small<T, NI>(b, st, small);
     const int64_t gstride = (int64_t)gridDim.x * kBlock;
     int64_t tid0 = (int64_t)blockIdx.x * kBlock;
     for (; tid0 < b.n_tiles; tid0 += gstride) {
         const int64_t tid = tid0 + threadIdx.x;
         T acc[V1 * V2];
         int64_t oo = 0;
-        if (tid < b.n_tiles) (void)compute_stream_tile<T, V1, V2, BC, true>(b, st, small, tid, acc, oo);
+        if (tid < b.n_tiles) (void)compute_stream_tile<T, V1, V2, BC, true, NI>(b, st, small, tid, acc, oo);
         stream_store<T, V1, V2, BC>(b, tid0, tid, oo, acc, stage);
     }
 }
@@ -991,21 +995,21 @@ static hipError_t go_single(const SingleArgs &a, int max_grid, hipStream_t strea
     return hipGetLastError();
 }
 
-template <typename T, int V1, int V2, int BC>
+template <typename T, int V1, int V2, int BC, int NI = kStreamMaxIn>
 static hipError_t go_stream_level(const LevelArgs &a, int small_elems, int max_grid, hipStream_t stream) {
     int64_t grid = a.vblocks < max_grid ? a.vblocks : max_grid;
     size_t shm = kRedBytes + (kBlock / 64) * kLdsWaveBytes + (size_t)small_elems * sizeof(T);
-    hipLaunchKernelGGL((stream_level_kernel<T, V1, V2, BC>), dim3((unsigned)grid), dim3(kBlock), shm, stream, a.descs,
+    hipLaunchKernelGGL((stream_level_kernel<T, V1, V2, BC, NI>), dim3((unsigned)grid), dim3(kBlock), shm, stream, a.descs,
                        a.n_desc, a.pool, a.meta, a.vblocks);
     return hipGetLastError();
 }
 
-template <typename T, int V1, int V2, int BC>
+template <typename T, int V1, int V2, int BC, int NI = kStreamMaxIn>
 static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_t stream) {
     int64_t blocks = (a.d.n_tiles + kBlock - 1) / kBlock;
     int64_t grid = blocks < max_grid ? blocks : max_grid;
     size_t shm = kRedBytes + (kBlock / 64) * kLdsWaveBytes + (size_t)a.d.small_elems * sizeof(T);
-    hipLaunchKernelGGL((stream_single_kernel<T, V1, V2, BC>), dim3((unsigned)grid), dim3(kBlock), shm, stream, a);
+    hipLaunchKernelGGL((stream_single_kernel<T, V1, V2, BC, NI>), dim3((unsigned)grid), dim3(kBlock), shm, stream, a);
     return hipGetLastError();
 }
 
@@ -1022,6 +1026,16 @@ static hipError_t go_stream_single(const SingleArgs &a, int max_grid, hipStream_
     case 4096 + BC * 256 + V1 * 16 + V2: return go_stream_level<T, V1, V2, BC>(a, small_elems, max_grid, stream);
 #define BNPP_CASE_SSINGLE(T, V1, V2, BC) \
     case 4096 + BC * 256 + V1 * 16 + V2: return go_stream_single<T, V1, V2, BC>(a, max_grid, stream);
+// 5-8 inputs (kStream8In): the direct big classes over the plain tiles, no interleaved forms
+#define BNPP_STREAM8_BC(X, T, V1, V2) X(T, V1, V2, 1) X(T, V1, V2, 2) X(T, V1, V2, 3) X(T, V1, V2, 4) X(T, V1, V2, 5)
+#define BNPP_STREAM8_F32(X, T) BNPP_STREAM8_BC(X, T, 1, 1) BNPP_STREAM8_BC(X, T, 2, 1) BNPP_STREAM8_BC(X, T, 4, 1) \
+    BNPP_STREAM8_BC(X, T, 2, 2) BNPP_STREAM8_BC(X, T, 2, 4) BNPP_STREAM8_BC(X, T, 4, 2) BNPP_STREAM8_BC(X, T, 4, 4)
+#define BNPP_STREAM8_F64(X, T) BNPP_STREAM8_BC(X, T, 1, 1) BNPP_STREAM8_BC(X, T, 2, 1) BNPP_STREAM8_BC(X, T, 4, 1) \
+    BNPP_STREAM8_BC(X, T, 2, 2) BNPP_STREAM8_BC(X, T, 2, 4) BNPP_STREAM8_BC(X, T, 4, 2)
+#define BNPP_CASE_SLEVEL8(T, V1, V2, BC) \
+    case 4096 + kStream8In + BC * 256 + V1 * 16 + V2: return go_stream_level<T, V1, V2, BC, 8>(a, small_elems, max_grid, stream);
+#define BNPP_CASE_SSINGLE8(T, V1, V2, BC) \
+    case 4096 + kStream8In + BC * 256 + V1 * 16 + V2: return go_stream_single<T, V1, V2, BC, 8>(a, max_grid, stream);
 
 // (3, 1) (5, 1) (6, 1) (7, 1): a whole fastest dim of that card per thread
 #define BNPP_TILES_ODD(X, T, NIN) X(T, NIN, 3, 1) X(T, NIN, 5, 1) X(T, NIN, 6, 1) X(T, NIN, 7, 1)

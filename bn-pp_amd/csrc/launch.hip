@@ -57,18 +57,18 @@ hipError_t launch_copies(const CopyItem *items, int n, int64_t max_bytes, hipStr
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream) {
     if (a.d.n_tiles <= 0) return hipSuccess;
     if (a.d.big >= 0 && a.d.bcls == kBigSlab) {
-        const int key = slab_key(a.d.k, a.d.v1, a.d.v2, a.d.lanes);
+        const int key = slab_key(a.d.k, a.d.v1, a.d.v2, a.d.lanes, 1, a.d.n_in);
         return is_f32 ? dispatch_slab_single_f32(key, a, stream) : dispatch_slab_single_f64(key, a, stream);
     }
     if (a.d.big >= 0) {
-        const int key = stream_key(a.d.bcls, a.d.v1, a.d.v2);
+        const int key = stream_key(a.d.bcls, a.d.v1, a.d.v2, a.d.n_in);
         return is_f32 ? dispatch_stream_single_f32(key, a, max_grid, stream)
                       : dispatch_stream_single_f64(key, a, max_grid, stream);
     }
     int64_t in_bytes = 0;
     for (int i = 0; i < a.d.n_in && i < kMaxIn; ++i)
         in_bytes = std::max<int64_t>(in_bytes, a.meta[i].size * (is_f32 ? 4 : 8));
-    const int key = variant_key(a.d.n_in, a.d.v1, a.d.v2) + (generic_o32(in_bytes) ? kGenericO32 : 0);
+    const int key = variant_key(a.d.n_in, a.d.v1, a.d.v2) + (generic_o32(in_bytes) ? kGenericO32 : 0);   // plan.hpp generic_variant
     return is_f32 ? dispatch_single_f32(key, a, max_grid, stream) : dispatch_single_f64(key, a, max_grid, stream);
 }
 

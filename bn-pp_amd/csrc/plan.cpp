@@ -650,7 +650,9 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
         const char *os = tuning_knob("BNPP_ODD_STREAM");                 // A/B knob: 1 = keep the stream form
         const bool odd_rows = v1 == 1 && (c0 == 3 || c0 == 5 || c0 == 7 || (c0 == 6 && aligned(0, 2))) && (int)c0 <= max_tile &&
                               !(os && *os == '1');
-        if (!b.simple && !b.divide && n_big == 1 && n <= 4 && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 &&
+        // 5-8 inputs: their own stream instantiations (kStream8In), every tile but 2x8
+        const bool nin_ok = n <= 4 || (n <= kMaxIn && !(v1 == 2 && v2 == 8));
+        if (!b.simple && !b.divide && n_big == 1 && nin_ok && small_total * eb <= kStreamLdsBudget && d.n_tiles >= 1024 &&
             !(off && *off == '1') && !odd_rows) {
             int64_t s0 = merged.empty() ? 0 : merged[0].s[big];
             int64_t s1 = merged.size() < 2 ? 0 : merged[1].s[big];
@@ -668,6 +670,12 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 const char *no = std::getenv("BNPP_NO_SLAB_OUTER");
                 if (!merged.empty() && merged[0].s[big] == 1) slab_dim = 0;
                 else if (merged.size() >= 2 && merged[0].s[big] == 0 && merged[1].s[big] == 1) slab_dim = 1;
+                // a row over two binary dims the big input does not vary along
+                // (slab_y2): the conditioned 32x32 PR's 5-input bucket
+                // [2][2][2^29 slab][2], 46 ms on the generic kernel
+                else if (merged.size() >= 3 && merged[0].s[big] == 0 && merged[1].s[big] == 0 && merged[2].s[big] == 1 &&
+                         merged[0].card == 2 && merged[1].card == 2)
+                    slab_dim = 2;
                 if (slab_dim >= 0)
                     for (size_t j = (size_t)slab_dim + 1; j < merged.size(); ++j)
                         slab_outer_n = sat_mul(slab_outer_n, (int64_t)merged[j].card);
@@ -682,8 +690,11 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                                          (slab_dim == 1 && (int64_t)merged[0].card > max_c0)))
                     slab_dim = -1;
                 const Dim *sd = slab_dim >= 0 ? &merged[slab_dim] : nullptr;
-                slab_c0 = slab_dim == 1 ? (int)merged[0].card : 1;
-                bool ok = !(ns && *ns == '1') && sd && k >= 1 && k <= 4 && (slab_c0 == 1 || slab_c0 == 2 || slab_c0 == 4);
+                slab_c0 = slab_dim == 1 ? (int)merged[0].card : slab_dim == 2 ? 4 : 1;
+                // (slab kernels: up to 4 inputs in every shape, 5-8 with one
+                // slab entry per lane -- slab.cuh kSlabMaxIn / BNPP_SLAB8_*)
+                bool ok = !(ns && *ns == '1') && sd && n <= kMaxIn && k >= 1 && k <= 4 &&
+                          (slab_c0 == 1 || slab_c0 == 2 || slab_c0 == 4);
                 for (int i = 0; ok && i < n; ++i)
                     if (i != big && sd->s[i] != 0) ok = false;
                 if (ok) {
@@ -696,6 +707,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                                           (want == 2 && eb == 8 && slab_c0 == 1) || (want == 4 && eb == 4 && slab_c0 == 1);
                         if (inst) vn = want;
                     }
+                    if (n > 4) vn = 1;                              // the 5-8-input instantiations
                     if ((int64_t)sd->card % vn || b.in[big].base % vn || es[big] % vn) vn = 1;
                     for (size_t j = (size_t)slab_dim + 1; j < merged.size(); ++j)
                         if (merged[j].s[big] % vn) vn = 1;
@@ -720,6 +732,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                 d.n_tiles = out_size / (v1 * v2);
                 d.big = big;
                 d.bcls = kBigSlab;
+                d.slab_y2 = slab_dim == 2 ? 2 : 0;
                 // 32-B rows (f64 c0 * v = 4, f32 8): two lanes per tile, 16 B each
                 const char *sl = tuning_knob("BNPP_SLAB_LANES");     // A/B knob: 1 = one lane per tile
                 d.lanes = v1 * v2 * eb == 32 && !(sl && *sl == '1') ? 2 : 1;
@@ -735,7 +748,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     const char *sr = tuning_knob("BNPP_SLAB_R");          // A/B knob: 1 = one pass
                     const bool inst = d.lanes == 1 && ((eb == 4 && ((v1 == 1 && v2 == 4) || (v1 == 2 && v2 == 2))) ||
                                                        (eb == 8 && v1 == 1 && v2 == 2));
-                    if (slab_outer && !(sr && std::atoi(sr) == 1) && inst &&
+                    if (slab_outer && !(sr && std::atoi(sr) == 1) && inst && n <= 4 &&
                         (slab_outer_n == 1 || ((int64_t)merged[slab_dim].card / v2) % (2 * kBlock) == 0))
                         d.slab_r = 2;
                 }
@@ -773,7 +786,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
             // interleaved: the summed variable is the big input's fastest dim and
             // output dim 0 follows it, so a V1-entry tile reads V1*k contiguous values
             bool inter = false;
-            if ((k == 2 || k == 4) && es[big] == 1 && s0 == k && v1 >= 2 && !merged.empty()) {
+            if (n <= 4 && (k == 2 || k == 4) && es[big] == 1 && s0 == k && v1 >= 2 && !merged.empty()) {
                 const int64_t vw = 16 / eb;
                 inter = b.in[big].base % vw == 0 && (int64_t)(v1 * k) % vw == 0;
                 for (size_t j = 1; inter && j < merged.size(); ++j)
@@ -2168,6 +2181,120 @@ struct Arena {
         add_free(off, n);
     }
 };
+
+// Place the tables of one arena level by level (born_at[L] allocated, then
+// dies_at[L] released): off[t - t_base] for every table t placed.  Two
+// placements are made and the one with the lower top kept: (a) one best-fit
+// arena; (b) the tables of the largest size first, by interval colouring into
+// K slots of that size (K = the most of them live at once: no fragmentation
+// among them), then every smaller table, in level order, into a slot that no
+// large table occupies during its whole lifetime (a best-fit arena per slot),
+// or else into a region above the slots.  In one arena a small table left in
+// a freed message's hole can leave the next message no room -- the fp64
+// 32x32 bucket tree with four checkpoint slots: 240.8 GB live at its peak,
+// 275.0 GB placed in one arena (one 34-GB message more).
+template <class Bytes>
+int64_t place_levels(int n_levels, const std::vector<std::vector<int>> &born_at,
+                     const std::vector<std::vector<int>> &dies_at, Bytes &&bytes, int t_base, std::vector<int64_t> &off,
+                     bool &saturated) {
+    auto rnd = [](int64_t n) { return (n + 255) & ~(int64_t)255; };
+    int64_t big = 0;
+    size_t n_tab = 0;
+    for (int L = 1; L <= n_levels; ++L) {
+        n_tab += born_at[L].size();
+        for (int t : born_at[L]) big = std::max(big, rnd(bytes(t)));
+    }
+    Arena one;
+    for (int L = 1; L <= n_levels; ++L) {
+        for (int t : born_at[L]) off[t - t_base] = one.alloc(bytes(t));
+        for (int t : dies_at[L]) one.release(off[t - t_base], bytes(t));
+    }
+    saturated = one.saturated;
+    // (b) only where a large table exists beside others and the walk stays cheap
+    if (one.saturated || big <= 0 || one.top <= big || big >= kSatMax / 4 || n_tab > 50000) return one.top;
+    const int kLive = INT_MAX;
+    std::vector<int> die(off.size(), kLive);
+    for (int L = 1; L <= n_levels; ++L)
+        for (int t : dies_at[L]) die[t - t_base] = L;
+    auto is_big = [&](int t) { return rnd(bytes(t)) == big; };
+    // large tables: interval colouring (allocations of a level before its releases)
+    std::vector<int> slot(off.size(), -1);
+    std::vector<std::vector<std::pair<int, int>>> busy;          // per slot: (born, dies) of its large tables
+    std::vector<int> free_slots;                                 // a min-heap of slot ids
+    for (int L = 1; L <= n_levels; ++L) {
+        for (int t : born_at[L]) {
+            if (!is_big(t)) continue;
+            int k;
+            if (!free_slots.empty()) {
+                std::pop_heap(free_slots.begin(), free_slots.end(), std::greater<int>());
+                k = free_slots.back();
+                free_slots.pop_back();
+            } else {
+                k = (int)busy.size();
+                busy.emplace_back();
+            }
+            slot[t - t_base] = k;
+            busy[k].push_back({L, die[t - t_base]});
+        }
+        for (int t : dies_at[L]) {
+            if (!is_big(t)) continue;
+            free_slots.push_back(slot[t - t_base]);
+            std::push_heap(free_slots.begin(), free_slots.end(), std::greater<int>());
+        }
+    }
+    const int K = (int)busy.size();
+    std::vector<Arena> in_slot(K);
+    Arena above;
+    std::vector<int64_t> off2(off.size(), 0);
+    for (int L = 1; L <= n_levels; ++L) {
+        for (int t : born_at[L]) {
+            const int i = t - t_base;
+            if (is_big(t)) {
+                off2[i] = (int64_t)slot[i] * big;
+                continue;
+            }
+            const int64_t n = bytes(t);
+            const int d = die[i];
+            int got = -1;
+            for (int k = 0; k < K && got < 0; ++k) {
+                bool clear = true;
+                for (const auto &iv : busy[k])
+                    if (iv.first <= d && L <= iv.second) {
+                        clear = false;
+                        break;
+                    }
+                if (!clear) continue;
+                const int64_t o = in_slot[k].alloc(n);
+                if (o + rnd(n) <= big) {
+                    got = k;
+                    off2[i] = (int64_t)k * big + o;
+                } else {
+                    in_slot[k].release(o, n);
+                }
+            }
+            if (got < 0) {
+                slot[i] = -2;                               // above the slots
+                off2[i] = above.alloc(n);
+            } else {
+                slot[i] = got;
+            }
+        }
+        for (int t : dies_at[L]) {
+            const int i = t - t_base;
+            if (is_big(t)) continue;
+            if (slot[i] == -2) above.release(off2[i], bytes(t));
+            else in_slot[slot[i]].release(off2[i] - (int64_t)slot[i] * big, bytes(t));
+        }
+    }
+    const int64_t base_above = (int64_t)K * big;
+    if (above.saturated || sat_add(base_above, above.top) >= one.top) return one.top;
+    for (int L = 1; L <= n_levels; ++L)
+        for (int t : born_at[L]) {
+            const int i = t - t_base;
+            off[i] = slot[i] == -2 ? base_above + off2[i] : off2[i];
+        }
+    return base_above + above.top;
+}
 }  // namespace
 
 int64_t plan_arena_bytes(const VEPlan &p, int elem_bytes) {
@@ -2187,14 +2314,20 @@ int64_t plan_arena_bytes(const VEPlan &p, int elem_bytes) {
         born_at[born[t]].push_back(t);
         if (!keep[t]) dies_at[std::max(last[t], born[t])].push_back(t);
     }
-    Arena arena;
     std::vector<int64_t> off(nt, 0);
     auto bytes = [&](int t) { return sat_mul(p.msgs[t - p.n_src].size, elem_bytes); };
-    for (int L = 1; L <= p.n_levels; ++L) {
-        for (int t : born_at[L]) off[t] = arena.alloc(bytes(t));
-        for (int t : dies_at[L]) arena.release(off[t], bytes(t));
+    bool sat = false;
+    const int64_t top = place_levels(p.n_levels, born_at, dies_at, bytes, 0, off, sat);
+    if (std::getenv("BNPP_DEBUG_ARENA")) {
+        int64_t live = 0, peak = 0;
+        for (int L = 1; L <= p.n_levels; ++L) {
+            for (int t : born_at[L]) live += bytes(t);
+            peak = std::max(peak, live);
+            for (int t : dies_at[L]) live -= bytes(t);
+        }
+        std::fprintf(stderr, "[bnpp] arena %.2f GB, ideal live peak %.2f GB\n", top / 1e9, peak / 1e9);
     }
-    return arena.top;
+    return sat ? kSatMax : top;
 }
 
 bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<int> &cards,
@@ -2429,13 +2562,13 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                 ba[born[t]].push_back(t);
                 if (last[t] != kForever) da[std::max(last[t], born[t])].push_back(t);
             }
-            Arena a;
-            for (int L = 1; L <= n_levels; ++L) {
-                for (int t : ba[L]) offs[t] = a.alloc(sat_mul(s.table_size[t], elem_bytes));
-                for (int t : da[L]) a.release(offs[t], sat_mul(s.table_size[t], elem_bytes));
-            }
-            tops[pi] = a.top;
-            sat[pi] = a.saturated;
+            std::vector<int64_t> lo(t1 - t0, 0);
+            bool st = false;
+            tops[pi] = place_levels(n_levels, ba, da, [&](int t) { return sat_mul(s.table_size[t], elem_bytes); }, t0,
+                                    lo, st);
+            for (int L = 1; L <= n_levels; ++L)
+                for (int t : ba[L]) offs[t] = lo[t - t0];
+            sat[pi] = st;
         });
         int64_t total = 0;
         bool any_sat = false;
@@ -2456,18 +2589,26 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         }
     }
     if (!placed) {
-        std::vector<Arena> arenas(n_lanes);
-        for (int L = 1; L <= n_levels; ++L) {
-            for (int t : born_at[L]) s.table_offset[t] = arenas[lane_of[t]].alloc(sat_mul(s.table_size[t], elem_bytes));
-            for (int t : dies_at[L]) arenas[lane_of[t]].release(s.table_offset[t], sat_mul(s.table_size[t], elem_bytes));
-        }
         int64_t base = 0;
         bool sat = false;
         std::vector<int64_t> lane_base(n_lanes, 0);
         for (int l = 0; l < n_lanes; ++l) {
+            std::vector<std::vector<int>> ba(n_levels + 2), da(n_levels + 2);
+            for (int L = 0; L < n_levels + 2; ++L) {
+                for (int t : born_at[L])
+                    if (lane_of[t] == l) ba[L].push_back(t);
+                for (int t : dies_at[L])
+                    if (lane_of[t] == l) da[L].push_back(t);
+            }
+            std::vector<int64_t> lo(s.n_tables - s.n_src, 0);
+            bool st = false;
+            const int64_t top = place_levels(n_levels, ba, da, [&](int t) { return sat_mul(s.table_size[t], elem_bytes); },
+                                             s.n_src, lo, st);
+            for (int L = 1; L <= n_levels; ++L)
+                for (int t : ba[L]) s.table_offset[t] = lo[t - s.n_src];
             lane_base[l] = base;
-            base = sat_add(base, arenas[l].top);
-            sat = sat || arenas[l].saturated;
+            base = sat_add(base, top);
+            sat = sat || st;
         }
         if (n_lanes > 1)
             for (int t = s.n_src; t < s.n_tables; ++t)
@@ -2539,11 +2680,10 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         };
         it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf) +
                                   ((it.d.flags & kChainBel) ? kChainBelKey : 0)
-                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes, it.d.slab_r)
-                 : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2)
-                 : (b.simple ? variant_key(kMaxIn, 1, 1)        // the widest input class runs any input count
-                             : variant_key(it.d.n_in, it.d.v1, it.d.v2)) +
-                       (generic_o32(max_in_bytes(b)) && !no_o32 ? kGenericO32 : 0);
+                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes, it.d.slab_r, it.d.n_in)
+                 : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2, it.d.n_in)
+                 : b.simple ? generic_variant(kMaxIn, 1, 1, max_in_bytes(b), no_o32)   // the widest input class runs any input count
+                            : generic_variant(it.d.n_in, it.d.v1, it.d.v2, max_in_bytes(b), no_o32);
     });
     const double T2 = clk();
     for (const Item &it : items)

@@ -64,6 +64,19 @@ inline int64_t sat_add(int64_t a, int64_t b) {
     int64_t r;
     return __builtin_add_overflow(a, b, &r) || r > kSatMax ? kSatMax : r;
 }
+// entries a view can reach from its table's start (base + the last entry's
+// offset + 1): what the 32-bit-offset generic kernels are chosen by
+inline int64_t view_span(const View &v, const std::vector<int> &cards) {
+    int64_t span = sat_add(v.base, 1);
+    for (size_t j = 0; j < v.vars.size() && j < v.strides.size(); ++j)
+        span = sat_add(span, sat_mul(cards[v.vars[j]] - 1, v.strides[j]));
+    return span;
+}
+// generic-kernel variant of a bucket whose largest input view reaches
+// max_in_bytes: the 32-bit-offset kernels only when every offset fits
+inline int generic_variant(int n_in, int v1, int v2, int64_t max_in_bytes, bool no_o32 = false) {
+    return variant_key(n_in, v1, v2) + (generic_o32(max_in_bytes) && !no_o32 ? kGenericO32 : 0);
+}
 std::vector<int64_t> natural_strides(const std::vector<int> &vars, const std::vector<int> &cards);
 int64_t table_size(const std::vector<int> &vars, const std::vector<int> &cards);
 View natural_view(int table, const std::vector<int> &vars, const std::vector<int> &cards);

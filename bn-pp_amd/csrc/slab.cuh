@@ -29,19 +29,25 @@
 
 namespace bnpp {
 
-constexpr int kSlabMaxIn = 4;
+constexpr int kSlabMaxIn = 4;       // inputs of the default class; NI = 8: buckets of 5-8 inputs (kSlab8In)
 
 // tile outputs per lane: C0 * V consecutive entries
-template <typename T, int K, int C0, int V>
+template <typename T, int K, int C0, int V, int NI = kSlabMaxIn>
 struct SlabTile {
     static constexpr int N = C0 * V;
 
-    // small input i's values at (v, y) -> g[v][y] (wave-uniform loads)
-    static __device__ __forceinline__ void load_small(const T *p, int64_t es, int64_t sy, T (&g)[K][C0]) {
+    // small input i's values at (v, y) -> g[v][y] (wave-uniform loads); the
+    // row's y spans output dim 0 (stride sy) or, when y2 > 0, dims 0 and 1
+    // (y % y2 along dim 0, y / y2 along dim 1 at stride sy1; C0 = 4, y2 = 2)
+    static __device__ __forceinline__ void load_small(const T *p, int64_t es, int64_t sy, T (&g)[K][C0], int y2 = 0,
+                                                      int64_t sy1 = 0) {
 #pragma unroll
         for (int v = 0; v < K; ++v)
 #pragma unroll
-            for (int y = 0; y < C0; ++y) g[v][y] = gload(p + (int64_t)v * es + (int64_t)y * sy);
+            for (int y = 0; y < C0; ++y) {
+                const int64_t oy = y2 == 2 ? (int64_t)(y & 1) * sy + (int64_t)(y >> 1) * sy1 : (int64_t)y * sy;
+                g[v][y] = gload(p + (int64_t)v * es + oy);
+            }
     }
 
     // acc[j * C0 + y] for s = s0 + j:  inputs in chain order around the big one
@@ -51,7 +57,7 @@ struct SlabTile {
         T pre[K][C0];
         bool has_pre = false;
 #pragma unroll
-        for (int i = 0; i < kSlabMaxIn; ++i) {
+        for (int i = 0; i < NI; ++i) {
             if (i >= n_in || i >= big) break;               // uniform
             T g[K][C0];
             small(i, g);
@@ -69,7 +75,7 @@ struct SlabTile {
 #pragma unroll
                 for (int y = 0; y < C0; ++y) p[v][j * C0 + y] = has_pre ? pre[v][y] * m[v][j] : m[v][j];
 #pragma unroll
-        for (int i = 1; i < kSlabMaxIn; ++i) {
+        for (int i = 1; i < NI; ++i) {
             if (i >= n_in) break;                           // uniform
             if (i <= big) continue;
             T g[K][C0];
@@ -91,9 +97,13 @@ struct SlabTile {
     }
 };
 
-// stride of small input i along y (output dim 0 when C0 = v1 > 1)
+// stride of small input i along y (output dim 0 when C0 = v1 > 1), and along
+// output dim 1 when the row spans two dims (slab_y2)
 __device__ __forceinline__ int64_t slab_sy(const BucketDesc &d, const int64_t *dims, int i) {
     return d.v1 > 1 ? dims[2 + i] : 0;
+}
+__device__ __forceinline__ int64_t slab_sy1(const BucketDesc &d, const int64_t *dims, int i) {
+    return d.slab_y2 ? dims[(2 + d.n_in) + 2 + i] : 0;
 }
 
 template <typename T, int K, int C0, int V, bool NTL>
@@ -119,7 +129,7 @@ __device__ __forceinline__ void slab_store(T *row, const T (&acc)[N], int h) {
     }
 }
 
-template <typename T, int K, int C0, int V, int H>
+template <typename T, int K, int C0, int V, int H, int NI>
 __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs args) {
 #if defined(__HIP_DEVICE_COMPILE__)
     (void)args;
@@ -127,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs ar
 #else
     const SingleArgs &a = args;
 #endif
-    using ST = SlabTile<T, K, C0, V>;
+    using ST = SlabTile<T, K, C0, V, NI>;
     const BucketDesc &d = a.d;
     const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t t = H == 1 ? gt : gt / H;
@@ -137,7 +147,8 @@ __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs ar
     slab_load_big<T, K, C0, V, true>(static_cast<const T *>(a.big_ptr) + t * V, a.big_es, m);
     T acc[ST::N];
     ST::compute(m, big, d.n_in, [&](int i, T (&g)[K][C0]) {
-        ST::load_small(static_cast<const T *>(a.meta[i].ptr) + d.in_base[i], d.elim_stride[i], slab_sy(d, a.pool, i), g);
+        ST::load_small(static_cast<const T *>(a.meta[i].ptr) + d.in_base[i], d.elim_stride[i], slab_sy(d, a.pool, i), g,
+                       d.slab_y2, slab_sy1(d, a.pool, i));
     }, acc);
     slab_store<T, ST::N, H, true>(static_cast<T *>(a.meta[d.n_in].ptr) + t * ST::N, acc, (int)(gt & (H - 1)));
 }
@@ -145,11 +156,11 @@ __global__ __launch_bounds__(kBlock) void slab_single_kernel(const SingleArgs ar
 // Level form: one workgroup per virtual block of a level's slab buckets (flat
 // grid), with the VE rescaling (kScale) and the max tracking (kTrackMax) of
 // the other level kernels.
-template <typename T, int K, int C0, int V, int H, int R>
+template <typename T, int K, int C0, int V, int H, int R, int NI>
 __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__restrict__ descs, int n_desc,
                                                             const int64_t *__restrict__ pool,
                                                             TableMeta *__restrict__ meta) {
-    using ST = SlabTile<T, K, C0, V>;
+    using ST = SlabTile<T, K, C0, V, NI>;
     __shared__ T red[kBlock / 64];
     const int64_t vb = blockIdx.x;
     const int bi = n_desc == 1 ? 0 : find_bucket(descs, n_desc, vb);
@@ -177,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
                                                 d.elim_stride[big], m[r]);
     int64_t e_sum = 0, x_sum = 0;
 #pragma unroll
-    for (int i = 0; i < kSlabMaxIn; ++i) {
+    for (int i = 0; i < NI; ++i) {
         if (i >= d.n_in) break;
         const TableMeta &mi = meta[d.in_table[i]];
         const int e = FBits<T>::exponent(mi.maxbits);
@@ -197,7 +208,7 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
         T acc[ST::N];
         ST::compute(m[r], big, d.n_in, [&](int i, T (&g)[K][C0]) {
             ST::load_small(static_cast<const T *>(meta[d.in_table[i]].ptr) + base_of(i), d.elim_stride[i],
-                           slab_sy(d, dims, i), g);
+                           slab_sy(d, dims, i), g, d.slab_y2, slab_sy1(d, dims, i));
         }, acc);
         if (d.flags & kScale) {
 #pragma unroll
@@ -227,17 +238,17 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
     }
 }
 
-template <typename T, int K, int C0, int V, int H>
+template <typename T, int K, int C0, int V, int H, int NI = kSlabMaxIn>
 static hipError_t go_slab_single(const SingleArgs &a, hipStream_t stream) {
     const int64_t blocks = (a.d.n_tiles * H + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((slab_single_kernel<T, K, C0, V, H>), dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
+    hipLaunchKernelGGL((slab_single_kernel<T, K, C0, V, H, NI>), dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
     return hipGetLastError();
 }
 
-template <typename T, int K, int C0, int V, int H, int R>
+template <typename T, int K, int C0, int V, int H, int R, int NI = kSlabMaxIn>
 static hipError_t go_slab_level(const LevelArgs &a, hipStream_t stream) {
-    hipLaunchKernelGGL((slab_level_kernel<T, K, C0, V, H, R>), dim3((unsigned)a.vblocks), dim3(kBlock), 0, stream, a.descs,
-                       a.n_desc, a.pool, a.meta);
+    hipLaunchKernelGGL((slab_level_kernel<T, K, C0, V, H, R, NI>), dim3((unsigned)a.vblocks), dim3(kBlock), 0, stream,
+                       a.descs, a.n_desc, a.pool, a.meta);
     return hipGetLastError();
 }
 
@@ -260,5 +271,13 @@ static hipError_t go_slab_level(const LevelArgs &a, hipStream_t stream) {
 #define BNPP_SLAB_R2_F64(X, T) BNPP_SLAB_K(X, T, 1, 2, 1)
 #define BNPP_CASE_SLAB_LEVEL_R2(T, K, C0, V, H) \
     case slab_key(K, C0, V, H, 2): return go_slab_level<T, K, C0, V, H, 2>(a, stream);
+// 5-8 inputs (kSlab8In): one entry of the slab dim per lane (V = 1), one pass;
+// H = 2 where the tile row is 32 B (f64 C0 = 4)
+#define BNPP_SLAB8_F32(X, T) BNPP_SLAB_K(X, T, 1, 1, 1) BNPP_SLAB_K(X, T, 2, 1, 1) BNPP_SLAB_K(X, T, 4, 1, 1)
+#define BNPP_SLAB8_F64(X, T) BNPP_SLAB_K(X, T, 1, 1, 1) BNPP_SLAB_K(X, T, 2, 1, 1) BNPP_SLAB_K(X, T, 4, 1, 2)
+#define BNPP_CASE_SLAB8_SINGLE(T, K, C0, V, H) \
+    case slab_key(K, C0, V, H, 1, 8): return go_slab_single<T, K, C0, V, H, 8>(a, stream);
+#define BNPP_CASE_SLAB8_LEVEL(T, K, C0, V, H) \
+    case slab_key(K, C0, V, H, 1, 8): return go_slab_level<T, K, C0, V, H, 1, 8>(a, stream);
 
 }  // namespace bnpp

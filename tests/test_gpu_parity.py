@@ -277,6 +277,85 @@ def test_slab_form_buckets(ctx, k, c0, scards):
         assert max(abs(a - b) / abs(b) for a, b in zip(vals, want)) < 1e-6
 
 
+@pytest.mark.parametrize("n_small,big_at", [(4, 0), (4, 3), (5, 2), (7, 7), (6, 1)])
+def test_stream_buckets_five_to_eight_inputs(ctx, n_small, big_at):
+    """Stream form with 5-8 inputs (kStream8In: one big input streamed, 4-7
+    small ones from LDS) -- the conditioned 32x32 PR's 5-input bucket over an
+    8-GiB message.  Small inputs over the output's fastest dims, the summed
+    variable and a slow dim; the big one at every chain position.  fp64
+    bit-exact against the oracle (and its partition sum), fp32 1e-6."""
+    rng = random.Random(n_small * 10 + big_at)
+    x, a, b, z = 0, 1, 2, 3                       # summed var; fastest output dims a, b; slow dim z
+    mid = list(range(4, 15))                      # the big input's middle dims (>= 2^13 entries)
+    cards = {x: 2, a: 2, b: 2, z: 2}
+    for v in mid:
+        cards[v] = rng.choice([2, 3])
+    bs = [z] + mid + [x]
+    size = 1
+    for v in bs:
+        size *= cards[v]
+    big = (bs, [rng.uniform(0.5, 2.0) for _ in range(size)])
+    pool = [[x, a], [x, b], [z, x], [a], [b, x], [x], [a, b], [z, a]]
+    smalls = []
+    for i in range(n_small):
+        sc = pool[i % len(pool)]
+        n = 1
+        for v in sc:
+            n *= cards[v]
+        smalls.append((sc, [rng.uniform(0.5, 2.0) for _ in range(n)]))
+    ins = smalls[:big_at] + [big] + smalls[big_at:]
+    fs = [refcpu.Factor.new(sc, cards, v) for sc, v in ins]
+    ref = refcpu.bucket(fs, x, cards[x])
+    planned = [z] + mid + [b, a]
+    t = torch.tensor(ref.values, dtype=torch.float64).reshape([cards[v] for v in ref.scope])
+    want = t.permute([ref.scope.index(v) for v in planned]).reshape(-1).tolist()
+    scope, vals = run_bucket(ctx, bnpp.F64, cards, ins, x, out_vars=planned)
+    assert vals == want
+    scope, vals = run_bucket(ctx, bnpp.F32, cards, ins, x, out_vars=planned)
+    assert max(abs(p - q) / abs(q) for p, q in zip(vals, want)) < 1e-6
+    # the whole-table partition sum in the reference's (entry, value) order
+    scope, vals, psum2 = run_bucket(ctx, bnpp.F64, cards, ins, x, with_sum=True)
+    assert vals == ref.values and psum2 == ref.partition
+
+
+@pytest.mark.parametrize("n_small,big_at", [(1, 0), (3, 2), (4, 0), (4, 4), (5, 3), (7, 1)])
+def test_slab_rows_over_two_dims(ctx, n_small, big_at):
+    """Slab form whose tile row spans the output's two fastest (binary) dims,
+    which the big input does not vary along (slab_y2), with 2-8 inputs
+    (kSlab8In from 5): the big input holds x as slabs contiguous along the
+    output's slow index, the small inputs depend on (x, a, b).  fp64
+    bit-exact against the oracle, fp32 1e-6."""
+    rng = random.Random(700 + n_small * 10 + big_at)
+    x, a, b = 0, 1, 2
+    mid = list(range(3, 15))
+    cards = {x: 2, a: 2, b: 2}
+    for v in mid:
+        cards[v] = rng.choice([2, 3])
+    cards[mid[-1]] = 4                            # whole tiles: the slab dim is a multiple of 4
+    size = 2
+    for v in mid:
+        size *= cards[v]
+    big = ([x] + mid, [rng.uniform(0.5, 2.0) for _ in range(size)])
+    pool = [[x, a], [b, x], [a, b], [x], [x, a, b], [a], [b, a, x]]
+    smalls = []
+    for i in range(n_small):
+        sc = pool[i % len(pool)]
+        n = 1
+        for v in sc:
+            n *= cards[v]
+        smalls.append((sc, [rng.uniform(0.5, 2.0) for _ in range(n)]))
+    ins = smalls[:big_at] + [big] + smalls[big_at:]
+    fs = [refcpu.Factor.new(sc, cards, v) for sc, v in ins]
+    ref = refcpu.bucket(fs, x, cards[x])
+    planned = mid + [b, a]
+    t = torch.tensor(ref.values, dtype=torch.float64).reshape([cards[v] for v in ref.scope])
+    want = t.permute([ref.scope.index(v) for v in planned]).reshape(-1).tolist()
+    scope, vals = run_bucket(ctx, bnpp.F64, cards, ins, x, out_vars=planned)
+    assert vals == want
+    scope, vals = run_bucket(ctx, bnpp.F32, cards, ins, x, out_vars=planned)
+    assert max(abs(p - q) / abs(q) for p, q in zip(vals, want)) < 1e-6
+
+
 def test_slab_level_kernels_in_ve(ctx, monkeypatch, capfd):
     """Whole VE runs with fused sweep runs off: a 12x12 min-fill plan and a
     14x14 column sweep hold slab-form buckets (bcls 8 in the plan dump), run by

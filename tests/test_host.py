@@ -466,7 +466,9 @@ def test_plan_fuses_beliefs_and_shares_reduction_levels(capfd):
     assert n_fused >= 8 and err_p.count(" belief: ") == 0
     assert fused[3] == plain[3] - n_fused                # the belief buckets are gone
     assert fused[6] < plain[6]                           # one read of pi per fused belief
-    assert fused[1] == plain[1]                          # same arena
+    # the same arena to 0.1 % (the placement by size class, plan.cpp
+    # place_levels, may put the few small tables a fusion removes elsewhere)
+    assert abs(fused[1] - plain[1]) <= 1e-3 * plain[1]
     base = {"BNPP_KEEP_LOG2": "16", "BNPP_TREE_SLOTS": "4"}
     free, _ = stats(24, 8, base)
     seq, _ = stats(24, 8, dict(base, BNPP_NO_FREE_REDUCE="1"))
@@ -507,3 +509,46 @@ def test_plan_slab_outer_dims(capfd):
     assert any(" passes=2" in ln for ln in outer), outer          # level slab blocks: two passes of tiles
     assert " outer=" not in err_off
     assert on[3] == off[3] and on[6] == off[6] and on[1] == off[1]
+
+
+def test_generic_offset_width_at_4gib_boundary(tmp_path):
+    """The 32-bit-offset generic kernels are chosen exactly when a view's
+    reachable span fits 2^32 bytes (fp32 and fp64, plain and conditioned views,
+    saturated spans): tests/cpp/o32_keys.cpp, headers only, no allocation."""
+    import subprocess
+    exe = str(tmp_path / "o32_keys")
+    csrc = os.path.join(REPO, "bn-pp_amd", "csrc")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I" + csrc, os.path.join(REPO, "tests", "cpp", "o32_keys.cpp"),
+                    "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert "o32 keys ok" in out.stdout
+
+
+def test_arena_placement_reaches_the_live_peak(capfd):
+    """The fp64 32x32 column-sweep tree with four checkpoint slots holds at
+    most seven 34.36-GB messages at once (240.79 GB); one best-fit arena
+    placed it in 275.03 GB (small tables in freed messages' holes), the
+    placement by size class (plan.cpp place_levels) in the live peak itself,
+    so a 257.7-GB budget (85 % of an idle MI355X's free memory) plans four
+    slots instead of three: 34.27 TB of traffic instead of 36.92."""
+    import os
+    from bnpp import synth
+    m = bnpp.Model.from_dict(synth.ising_grid(32, 32, seed=0))
+    col = [r * 32 + c for c in range(32) for r in range(32)]
+    os.environ.update({"BNPP_MEM_BUDGET_GB": "1000", "BNPP_TREE_SLOTS": "4", "BNPP_DEBUG_ARENA": "1"})
+    try:
+        capfd.readouterr()
+        st = bnpp.plan_tree_part(m, 0, 1, {}, "mf", bnpp.F64, col)[1]
+        err = capfd.readouterr().err
+        os.environ.pop("BNPP_TREE_SLOTS")
+        os.environ["BNPP_MEM_BUDGET_GB"] = "257.7"
+        st_b = bnpp.plan_tree_part(m, 0, 1, {}, "mf", bnpp.F64, col)[1]
+    finally:
+        for k in ("BNPP_MEM_BUDGET_GB", "BNPP_TREE_SLOTS", "BNPP_DEBUG_ARENA"):
+            os.environ.pop(k, None)
+    line = [ln for ln in err.splitlines() if "ideal live peak" in ln][0]
+    top, peak = (float(x) for x in line.replace("[bnpp] arena ", "").replace(" GB, ideal live peak", "")
+                 .replace(" GB", "").split())
+    assert top == peak and abs(st[1] / 1e9 - 240.79) < 0.05, line
+    assert st_b[1] <= 257.7e9 and abs(st_b[6] - st[6]) < 1e9         # the budget now plans four slots
