@@ -318,7 +318,7 @@ def test_stream_buckets_five_to_eight_inputs(ctx, n_small, big_at):
     assert vals == ref.values and psum2 == ref.partition
 
 
-@pytest.mark.parametrize("n_small,big_at", [(1, 0), (3, 2), (4, 0), (4, 4), (5, 3), (7, 1)])
+@pytest.mark.parametrize("n_small,big_at", [(2, 0), (2, 1), (3, 2), (4, 0), (4, 4), (5, 3), (7, 1)])
 def test_slab_rows_over_two_dims(ctx, n_small, big_at):
     """Slab form whose tile row spans the output's two fastest (binary) dims,
     which the big input does not vary along (slab_y2), with 2-8 inputs
