@@ -147,7 +147,8 @@ __host__ __device__ inline int stream_key(int bcls, int v1, int v2, int n_in = 0
 }
 // slab kernels (slab.cuh): K summed values, C0 entries of output dim 0, V slow-dim entries per lane
 // and R passes of tiles per block (level launches, BucketDesc::slab_r: 1 or 2)
-// + kSlab8In for buckets of 5-8 inputs (their own instantiations: slab.cuh NI = 8)
+// + kSlab8In for buckets of 5-8 inputs and for rows over two output dims
+// (slab_y2; their own instantiations: slab.cuh NI = 8; pass n_in = 8 for those)
 constexpr int kSlab8In = 8192;
 __host__ __device__ constexpr int slab_key(int k, int c0, int v, int h = 1, int r = 1, int n_in = 0) {
     return 16384 + (n_in > 4 ? kSlab8In : 0) + k * 1024 + (r == 4 ? 512 : r == 2 ? 256 : 0) + c0 * 16 + v + (h == 2 ? 8 : 0);

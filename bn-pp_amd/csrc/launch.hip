@@ -57,7 +57,7 @@ hipError_t launch_copies(const CopyItem *items, int n, int64_t max_bytes, hipStr
 hipError_t launch_single(int is_f32, const SingleArgs &a, int max_grid, hipStream_t stream) {
     if (a.d.n_tiles <= 0) return hipSuccess;
     if (a.d.big >= 0 && a.d.bcls == kBigSlab) {
-        const int key = slab_key(a.d.k, a.d.v1, a.d.v2, a.d.lanes, 1, a.d.n_in);
+        const int key = slab_key(a.d.k, a.d.v1, a.d.v2, a.d.lanes, 1, a.d.slab_y2 ? 8 : a.d.n_in);
         return is_f32 ? dispatch_slab_single_f32(key, a, stream) : dispatch_slab_single_f64(key, a, stream);
     }
     if (a.d.big >= 0) {

@@ -707,7 +707,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                                           (want == 2 && eb == 8 && slab_c0 == 1) || (want == 4 && eb == 4 && slab_c0 == 1);
                         if (inst) vn = want;
                     }
-                    if (n > 4) vn = 1;                              // the 5-8-input instantiations
+                    if (n > 4 || slab_dim == 2) vn = 1;            // the 8-input-class instantiations
                     if ((int64_t)sd->card % vn || b.in[big].base % vn || es[big] % vn) vn = 1;
                     for (size_t j = (size_t)slab_dim + 1; j < merged.size(); ++j)
                         if (merged[j].s[big] % vn) vn = 1;
@@ -748,7 +748,7 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     const char *sr = tuning_knob("BNPP_SLAB_R");          // A/B knob: 1 = one pass
                     const bool inst = d.lanes == 1 && ((eb == 4 && ((v1 == 1 && v2 == 4) || (v1 == 2 && v2 == 2))) ||
                                                        (eb == 8 && v1 == 1 && v2 == 2));
-                    if (slab_outer && !(sr && std::atoi(sr) == 1) && inst && n <= 4 &&
+                    if (slab_outer && !(sr && std::atoi(sr) == 1) && inst && n <= 4 && slab_dim < 2 &&
                         (slab_outer_n == 1 || ((int64_t)merged[slab_dim].card / v2) % (2 * kBlock) == 0))
                         d.slab_r = 2;
                 }
@@ -2680,7 +2680,7 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
         };
         it.key = it.d.chain ? chain_key((it.d.chain >> 16) & 0xf, it.d.k, it.d.chain & 0xff, (it.d.chain >> 20) & 0xf) +
                                   ((it.d.flags & kChainBel) ? kChainBelKey : 0)
-                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes, it.d.slab_r, it.d.n_in)
+                 : it.d.big >= 0 && it.d.bcls == kBigSlab ? slab_key(it.d.k, it.d.v1, it.d.v2, it.d.lanes, it.d.slab_r, it.d.slab_y2 ? 8 : it.d.n_in)
                  : it.d.big >= 0 ? stream_key(it.d.bcls, it.d.v1, it.d.v2, it.d.n_in)
                  : b.simple ? generic_variant(kMaxIn, 1, 1, max_in_bytes(b), no_o32)   // the widest input class runs any input count
                             : generic_variant(it.d.n_in, it.d.v1, it.d.v2, max_in_bytes(b), no_o32);

@@ -37,15 +37,19 @@ struct SlabTile {
     static constexpr int N = C0 * V;
 
     // small input i's values at (v, y) -> g[v][y] (wave-uniform loads); the
-    // row's y spans output dim 0 (stride sy) or, when y2 > 0, dims 0 and 1
-    // (y % y2 along dim 0, y / y2 along dim 1 at stride sy1; C0 = 4, y2 = 2)
+    // row's y spans output dim 0 (stride sy) or -- the 8-input class only
+    // (NI = 8), when y2 > 0 -- dims 0 and 1 (y % 2 along dim 0, y / 2 along
+    // dim 1 at stride sy1; C0 = 4, y2 = 2).  The default class keeps the
+    // one-dim form: the bench bucket's kernel lost 5 % to the run-time select
     static __device__ __forceinline__ void load_small(const T *p, int64_t es, int64_t sy, T (&g)[K][C0], int y2 = 0,
                                                       int64_t sy1 = 0) {
 #pragma unroll
         for (int v = 0; v < K; ++v)
 #pragma unroll
             for (int y = 0; y < C0; ++y) {
-                const int64_t oy = y2 == 2 ? (int64_t)(y & 1) * sy + (int64_t)(y >> 1) * sy1 : (int64_t)y * sy;
+                int64_t oy = (int64_t)y * sy;
+                if constexpr (NI > kSlabMaxIn)
+                    if (y2 == 2) oy = (int64_t)(y & 1) * sy + (int64_t)(y >> 1) * sy1;
                 g[v][y] = gload(p + (int64_t)v * es + oy);
             }
     }
@@ -98,7 +102,8 @@ struct SlabTile {
 };
 
 // stride of small input i along y (output dim 0 when C0 = v1 > 1), and along
-// output dim 1 when the row spans two dims (slab_y2)
+// output dim 1 when the row spans two dims (slab_y2: launched as the 8-input
+// class whatever the input count, slab_key)
 __device__ __forceinline__ int64_t slab_sy(const BucketDesc &d, const int64_t *dims, int i) {
     return d.v1 > 1 ? dims[2 + i] : 0;
 }
