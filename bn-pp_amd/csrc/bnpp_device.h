@@ -38,7 +38,12 @@ constexpr int split_g_budget_bytes(int f, int eb = 4) {
                               : split_xch_bytes(f, eb) + split_img_bytes(f, eb));
 }
 constexpr int split_max_f(int) { return 8; }                    // longest split run (fp32 and fp64)
-constexpr int split_max_bel_f(int eb) { return eb == 4 ? 8 : 7; } // longest run forming a fused belief
+// longest run forming a fused belief; BNPP_F64_BEL8 (variant builds): fp64
+// runs of 8 forming one too (the aliased layout, chainsplit.cuh split_alias)
+#ifndef BNPP_F64_BEL8
+#define BNPP_F64_BEL8 0
+#endif
+constexpr int split_max_bel_f(int eb) { return eb == 4 || BNPP_F64_BEL8 ? 8 : 7; }
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 
 // One per table (source factor or message), resident in device memory.

@@ -310,7 +310,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 template <typename T, int MODE, int F>
 __host__ __device__ constexpr bool split_alias() {
     return sizeof(T) == 8 && (((BNPP_F64_ALIAS != 0 || F == 8) && MODE == 0) || (F == 8 && MODE == 2) ||
-                              (BNPP_F64_BEL_ALIAS != 0 && MODE == 1));
+                              ((BNPP_F64_BEL_ALIAS != 0 || F == 8) && MODE == 1));
 }
 template <int F, int EB, bool ALIAS>
 __host__ __device__ constexpr int split_tile_lds() {
@@ -935,7 +935,12 @@ static hipError_t go_chain_split(const LevelArgs &a, int small_elems, hipStream_
     X(T, F, 6, kChainBwd, 0, false, false) X(T, F, 6, kChainBwd, 1, false, false) \
     X(T, F, 7, kChainFwd, 0, true, false) X(T, F, 7, kChainFwd, 1, true, false) \
     X(T, F, 8, kChainBwd, 0, true, false) X(T, F, 8, kChainBwd, 1, true, false)
+#if BNPP_F64_BEL8
+#define BNPP_CHAIN_SPLIT_F64(X) BNPP_CHAIN_SPLIT_FD(X, double, 5) BNPP_CHAIN_SPLIT_FD(X, double, 6) \
+    BNPP_CHAIN_SPLIT_FD(X, double, 7) BNPP_CHAIN_SPLIT_FD(X, double, 8)
+#else
 #define BNPP_CHAIN_SPLIT_F64(X) BNPP_CHAIN_SPLIT_FD(X, double, 5) BNPP_CHAIN_SPLIT_FD(X, double, 6) \
     BNPP_CHAIN_SPLIT_FD(X, double, 7) BNPP_CHAIN_SPLIT_FD_NOBEL(X, double, 8)
+#endif
 
 }  // namespace bnpp

@@ -1552,14 +1552,18 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
     // positions, and the forward messages are only recomputed to reach those.
     // 2^24 kept entries (measured on the 32x32 column sweep: 2^21 -> 2^24 cuts
     // the plan from 14.6 to 13.3 TB and the MAR from 2.96 to 2.73 s; kept sets
-    // matter only for separators above 2^24 entries); fp64: 2^25, so a
-    // 32-wide separator's belief sums 7 variables, the longest fp64 split run
-    // (a delivery's belief is formed inside the backward run that ends there
-    // when that run's slots are the summed variables, attach_belief).
-    // BNPP_KEEP_LOG2 / BNPP_SLOW_LOG2 override them (tests use tiny values on
-    // small grids).
+    // matter only for separators above 2^24 entries).  A delivery's belief is
+    // formed inside the backward run that ends there when that run's slots
+    // are the summed variables (attach_belief): fp32 runs of 8, fp64 runs of
+    // at most 7, so fp64 beliefs of a 32-wide separator (8 summed variables)
+    // stay separate passes -- fp64 used 2^25 kept entries until round 6 to
+    // fuse them, but with four checkpoint slots (plan.cpp place_levels) 2^24
+    // moves 31.85 TB against 34.27 and the fp64 32x32 MAR runs 5.93 s against
+    // 6.44-6.50 (fused fp64 runs of 8, BNPP_F64_BEL8: 5.95 s;
+    // profiles/r06_f64_keep_ab.txt).  BNPP_KEEP_LOG2 / BNPP_SLOW_LOG2
+    // override them (tests use tiny values on small grids).
     const char *ke = std::getenv("BNPP_KEEP_LOG2"), *se = std::getenv("BNPP_SLOW_LOG2");
-    const int64_t kKeepMax = (int64_t)1 << (ke ? std::atoi(ke) : elem_bytes == 8 ? 25 : 24),
+    const int64_t kKeepMax = (int64_t)1 << (ke ? std::atoi(ke) : 24),
                   kSlowMax = (int64_t)1 << (se ? std::atoi(se) : 13);
     auto slow_part = [&](const std::vector<int> &sep) {     // slowest vars summed in the first pass
         std::vector<int> slow;
