@@ -536,7 +536,9 @@ def test_arena_placement_reaches_the_live_peak(capfd):
     from bnpp import synth
     m = bnpp.Model.from_dict(synth.ising_grid(32, 32, seed=0))
     col = [r * 32 + c for c in range(32) for r in range(32)]
-    os.environ.update({"BNPP_MEM_BUDGET_GB": "1000", "BNPP_TREE_SLOTS": "4", "BNPP_DEBUG_ARENA": "1"})
+    # (2^25 kept entries: the round-5 fp64 default the numbers above were taken with)
+    os.environ.update({"BNPP_MEM_BUDGET_GB": "1000", "BNPP_TREE_SLOTS": "4", "BNPP_DEBUG_ARENA": "1",
+                       "BNPP_KEEP_LOG2": "25"})
     try:
         capfd.readouterr()
         st = bnpp.plan_tree_part(m, 0, 1, {}, "mf", bnpp.F64, col)[1]
@@ -545,7 +547,7 @@ def test_arena_placement_reaches_the_live_peak(capfd):
         os.environ["BNPP_MEM_BUDGET_GB"] = "257.7"
         st_b = bnpp.plan_tree_part(m, 0, 1, {}, "mf", bnpp.F64, col)[1]
     finally:
-        for k in ("BNPP_MEM_BUDGET_GB", "BNPP_TREE_SLOTS", "BNPP_DEBUG_ARENA"):
+        for k in ("BNPP_MEM_BUDGET_GB", "BNPP_TREE_SLOTS", "BNPP_DEBUG_ARENA", "BNPP_KEEP_LOG2"):
             os.environ.pop(k, None)
     line = [ln for ln in err.splitlines() if "ideal live peak" in ln][0]
     top, peak = (float(x) for x in line.replace("[bnpp] arena ", "").replace(" GB, ideal live peak", "")
