@@ -751,6 +751,24 @@ bool build_desc(const BucketSpec &b, const std::vector<int> &cards, int max_vec,
                     if (slab_outer && !(sr && std::atoi(sr) == 1) && inst && n <= 4 && slab_dim < 2 &&
                         (slab_outer_n == 1 || ((int64_t)merged[slab_dim].card / v2) % (2 * kBlock) == 0))
                         d.slab_r = 2;
+                    // the 8-input class (5-8 inputs, or rows over two dims): one
+                    // slab entry per lane leaves a block 256 lanes x K loads of
+                    // 4-8 B beside its per-block setup (descriptor, exponents of
+                    // every input, the small tables by scalar loads); R passes
+                    // per block, every pass's loads issued first (instantiated:
+                    // R = 2, 4; level launches).  The conditioned 32x32 PR's
+                    // 5-input bucket: fp32 13.6 / 11.4 / 10.5 ms at R = 1 / 2 / 4
+                    // (9.7 with the setup through the scalar cache), fp64 (two
+                    // lanes per 32-B row) 27.3 / 28.9 / 35.7 ms -- fp64 keeps one
+                    // pass (profiles/r06_slab8_passes_ab.txt)
+                    if (slab_outer && (n > 4 || slab_dim == 2) && eb == 4 && !(sr && std::atoi(sr) == 1)) {
+                        const int want = sr ? std::atoi(sr) : 4;
+                        for (int r = want == 2 || want == 4 ? want : 4; r >= 2; r /= 2)
+                            if (slab_outer_n == 1 || ((int64_t)merged[slab_dim].card / v2) % (r * kBlock / d.lanes) == 0) {
+                                d.slab_r = r;
+                                break;
+                            }
+                    }
                 }
                 if (slab_outer_n > 1) {
                     const int64_t S = (int64_t)merged[slab_dim].card;

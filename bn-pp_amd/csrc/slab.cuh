@@ -169,33 +169,40 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
     __shared__ T red[kBlock / 64];
     const int64_t vb = blockIdx.x;
     const int bi = n_desc == 1 ? 0 : find_bucket(descs, n_desc, vb);
-    const BucketDesc &d = descs[bi];
-    const int64_t *dims = pool + d.dim_off;
+    // descriptor, dims pool and the inputs' metadata through the scalar cache
+    // (read-only while the launch runs; the one store below, the output's
+    // exp2, is never read back here): read as plain global memory, every use
+    // after that store re-read them, a chain of dependent scalar loads ahead
+    // of each pass's big loads (the 8-input class's 5-input bucket of the
+    // conditioned 32x32 PR: 13.6 ms fp32 for 25.8 GB)
+    cst_t<BucketDesc> &d = *as_const(descs + bi);
+    cst_t<int64_t> *dims = as_const(pool) + d.dim_off;
+    cst_t<TableMeta> *cmeta = as_const(meta);
     const int big = d.big;
     // H lanes per tile; R passes of kBlock / H tiles per block, every pass's
     // loads issued before the first tile is computed
     constexpr int TPP = kBlock / H;
     const int64_t t0 = (vb - d.vblk_begin) * (TPP * R) + threadIdx.x / H;
     // outer dims: this block's combination (uniform) moves every input's base
-    const int64_t *adj = nullptr;
+    cst_t<int64_t> *adj = nullptr;
     if (d.outer_n > 0) {
         uint64_t q, r;
         divmod_dim((uint64_t)(vb - d.vblk_begin), d.outer_div[0], d.outer_div[1], q, r);
         adj = dims + d.outer_rel + (int64_t)q * d.n_in;
     }
     auto base_of = [&](int i) { return adj ? d.in_base[i] + adj[i] : d.in_base[i]; };
+    const T *bigp = static_cast<const T *>(cmeta[d.in_table[big]].ptr) + base_of(big);
+    const int64_t big_es = d.elim_stride[big];
     T m[R][K][V];
 #pragma unroll
     for (int r = 0; r < R; ++r)
         if (t0 + r * TPP < d.n_tiles)
-            slab_load_big<T, K, C0, V, kNtLoad>(static_cast<const T *>(meta[d.in_table[big]].ptr) + base_of(big) +
-                                                    (t0 + r * TPP) * V,
-                                                d.elim_stride[big], m[r]);
+            slab_load_big<T, K, C0, V, kNtLoad>(bigp + (t0 + r * TPP) * V, big_es, m[r]);
     int64_t e_sum = 0, x_sum = 0;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
         if (i >= d.n_in) break;
-        const TableMeta &mi = meta[d.in_table[i]];
+        cst_t<TableMeta> &mi = cmeta[d.in_table[i]];
         const int e = FBits<T>::exponent(mi.maxbits);
         if (d.flags & kScale) {
             e_sum += e;
@@ -212,8 +219,8 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
         if (t >= d.n_tiles) break;
         T acc[ST::N];
         ST::compute(m[r], big, d.n_in, [&](int i, T (&g)[K][C0]) {
-            ST::load_small(static_cast<const T *>(meta[d.in_table[i]].ptr) + base_of(i), d.elim_stride[i],
-                           slab_sy(d, dims, i), g, d.slab_y2, slab_sy1(d, dims, i));
+            ST::load_small(static_cast<const T *>(cmeta[d.in_table[i]].ptr) + base_of(i), d.elim_stride[i],
+                           d.v1 > 1 ? dims[2 + i] : 0, g, d.slab_y2, d.slab_y2 ? dims[(2 + d.n_in) + 2 + i] : 0);
         }, acc);
         if (d.flags & kScale) {
 #pragma unroll
@@ -221,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void slab_level_kernel(const BucketDesc *__
         }
 #pragma unroll
         for (int e = 0; e < ST::N; ++e) lmax = acc[e] > lmax ? acc[e] : lmax;
-        slab_store<T, ST::N, H, kNtStore>(static_cast<T *>(meta[d.out_table].ptr) + t * ST::N, acc,
+        slab_store<T, ST::N, H, kNtStore>(static_cast<T *>(cmeta[d.out_table].ptr) + t * ST::N, acc,
                                            (int)(threadIdx.x & (H - 1)));
     }
     if (d.flags & kTrackMax) {
@@ -283,6 +290,8 @@ static hipError_t go_slab_level(const LevelArgs &a, hipStream_t stream) {
 #define BNPP_CASE_SLAB8_SINGLE(T, K, C0, V, H) \
     case slab_key(K, C0, V, H, 1, 8): return go_slab_single<T, K, C0, V, H, 8>(a, stream);
 #define BNPP_CASE_SLAB8_LEVEL(T, K, C0, V, H) \
-    case slab_key(K, C0, V, H, 1, 8): return go_slab_level<T, K, C0, V, H, 1, 8>(a, stream);
+    case slab_key(K, C0, V, H, 1, 8): return go_slab_level<T, K, C0, V, H, 1, 8>(a, stream); \
+    case slab_key(K, C0, V, H, 2, 8): return go_slab_level<T, K, C0, V, H, 2, 8>(a, stream); \
+    case slab_key(K, C0, V, H, 4, 8): return go_slab_level<T, K, C0, V, H, 4, 8>(a, stream);
 
 }  // namespace bnpp
