@@ -1871,7 +1871,10 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                 int tb = -1;                                   // one pass: sum the slow vars
                 if (slow_j.size() >= 2) {
                     // folded into the backward run that made pi_j, when it can be
-                    if (sbits == 0 && bel.size() == 2) tb = B.attach_belief(bel[1], bel[0], slow_j);
+                    // (sliced runs too: slow_j leaves out the slice variables,
+                    // and attach_belief checks that lam and pi share the run's
+                    // slicing and layout)
+                    if (bel.size() == 2) tb = B.attach_belief(bel[1], bel[0], slow_j);
                     if (tb < 0) {
                         std::vector<View> mg = bel;
                         int vv = B.merge_group(mg, slow_j);
@@ -1906,8 +1909,10 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
         const char *nbf = std::getenv("BNPP_NO_BEL_FUSE");
         const bool bel_fuse = !(nbf && *nbf == '1');
         auto bel_run = [&](int j) {
-            if (!bel_fuse || sbits != 0 || !multi.count(j) || B.chain_eb == 0) return 0;
-            const int f = (int)slow[j].size();
+            if (!bel_fuse || !multi.count(j) || B.chain_eb == 0) return 0;
+            int f = 0;                                         // the belief's summed variables on this rank
+            for (int v : slow[j])
+                if (!contains(Sof(win[j]), v)) ++f;
             return f >= 5 && f <= split_max_bel_f(B.chain_eb) ? f : 0;
         };
         auto deliver = [&](int i, const View &lam_j) {
@@ -2058,7 +2063,10 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
                     lam_cur = advance(lam_pos >= 0 ? &lam_cur : nullptr, lam_pos, j);
                     lam_pos = j;
                 } else {
-                    pi_down_to(j);
+                    // arriving second, the backward front ends its run at j with
+                    // the belief's summed variables as slots, so the belief forms
+                    // inside it (attach_belief; lam comes from the other lane)
+                    pi_down_to(j, seen[e.i] ? bel_run(j) : 0);
                 }
                 if (!seen[e.i]) {                              // first arrival: keep this front's message
                     seen[e.i] = 1;
@@ -2308,8 +2316,13 @@ int64_t place_levels(int n_levels, const std::vector<std::vector<int>> &born_at,
             else in_slot[slot[i]].release(off2[i] - (int64_t)slot[i] * big, bytes(t));
         }
     }
+    // near-ties (within 1 %) go to the slots: the messages then sit at
+    // multiples of their own size, where the split runs are fastest (§7 round 6)
     const int64_t base_above = (int64_t)K * big;
-    if (above.saturated || sat_add(base_above, above.top) >= one.top) return one.top;
+    if (std::getenv("BNPP_DEBUG_ARENA"))
+        std::fprintf(stderr, "[bnpp] placement: one arena %.2f GB, %d slots of %.2f GB + %.2f GB above\n", one.top / 1e9,
+                     K, big / 1e9, above.top / 1e9);
+    if (above.saturated || sat_add(base_above, above.top) > one.top + one.top / 100) return one.top;
     for (int L = 1; L <= n_levels; ++L)
         for (int t : born_at[L]) {
             const int i = t - t_base;
@@ -2628,6 +2641,13 @@ bool build_schedule(const std::vector<const VEPlan *> &plans, const std::vector<
                                              s.n_src, lo, st);
             for (int L = 1; L <= n_levels; ++L)
                 for (int t : ba[L]) s.table_offset[t] = lo[t - s.n_src];
+            // a lane's arena starts at a multiple of its largest table (up to
+            // 1 GiB): its messages keep the alignment place_levels gave them
+            int64_t big = 256;
+            for (int L = 1; L <= n_levels; ++L)
+                for (int t : ba[L]) big = std::max(big, sat_mul(s.table_size[t], elem_bytes));
+            big = std::min<int64_t>(big, (int64_t)1 << 30);
+            if (l > 0 && base % big) base = sat_add(base, big - base % big);
             lane_base[l] = base;
             base = sat_add(base, top);
             sat = sat || st;

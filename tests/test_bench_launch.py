@@ -88,6 +88,14 @@ def test_sliced_mar_becomes_the_headline_from_four_ranks():
     assert json.loads(json.dumps(line)) == line
 
 
+def test_slower_sliced_leg_stays_a_subfield():
+    import bench
+    line = _line()
+    bench.merge_sliced(line, {"wall_ms": 1300.0, "ok": True}, 4)
+    assert line["mar"]["wall_ms"] == 1200.0 and line["mar"]["sliced"]["wall_ms"] == 1300.0
+    assert "mar_segment" not in line
+
+
 def test_failed_sliced_leg_keeps_the_segment_headline():
     import bench
     line = _line()
