@@ -814,8 +814,8 @@ int create_job(bnpp_ctx *ctx, const bnpp_model *m, int kind, int n_ev, const int
     g_timing[7] = job->pg.arena_reused ? 1.0 : 0.0;
     g_timing[8] = job->pg.arena_alloc_ms;
     if (std::getenv("BNPP_TIMING"))
-        std::fprintf(stderr, "[bnpp] job: upload %.1f ms, program (arena %.2f GB) %.1f ms\n", t1 - t0,
-                     job->pg.arena_bytes / 1e9, now_ms() - t1);
+        std::fprintf(stderr, "[bnpp] job: upload %.1f ms, program (arena %.2f GB at %p) %.1f ms\n", t1 - t0,
+                     job->pg.arena_bytes / 1e9, job->pg.arena, now_ms() - t1);
     return BNPP_OK;
 }
 
