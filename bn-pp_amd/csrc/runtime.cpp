@@ -332,9 +332,18 @@ void free_executable(Context &ctx, Executable &ex) {
 }
 
 void drop_arena_cache(Context &ctx) {
-    if (ctx.arena_cache) (void)hipFree(ctx.arena_cache);
+    if (ctx.arena_cache) (void)hipFree(static_cast<char *>(ctx.arena_cache) - ctx.arena_cache_pad);
     ctx.arena_cache = nullptr;
     ctx.arena_cache_bytes = 0;
+    ctx.arena_cache_pad = 0;
+}
+
+// alignment of the arena's base: hipMalloc returns 32-MiB-aligned addresses
+// for arenas this size; BNPP_ARENA_ALIGN_MB (tuning builds) asks for more
+static int64_t arena_align() {
+    int64_t a = 0;
+    if (const char *e = tuning_knob("BNPP_ARENA_ALIGN_MB")) a = std::atoll(e) << 20;
+    return a > 0 ? a : 0;
 }
 
 int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &&batches, Program &pg,
@@ -358,11 +367,16 @@ int make_program(Context &ctx, const DeviceSources &src, std::vector<Schedule> &
         // whatever the size asked (tools/map_probe.hip,
         // profiles/r04_map_probe.log) -- so it is timed on its own
         const auto ta = std::chrono::steady_clock::now();
-        if ((err = hipMalloc(&pg.arena, (size_t)need)) != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
+        const int64_t al = arena_align();
+        void *raw = nullptr;
+        if ((err = hipMalloc(&raw, (size_t)(need + al))) != hipSuccess) return fail(ctx, err, "hipMalloc(arena)");
+        pg.arena_pad = al ? (int64_t)((al - (uintptr_t)raw % (uint64_t)al) % (uint64_t)al) : 0;
+        pg.arena = static_cast<char *>(raw) + pg.arena_pad;
         pg.arena_alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
         if (use_cache) {
             ctx.arena_cache = pg.arena;
             ctx.arena_cache_bytes = need;
+            ctx.arena_cache_pad = pg.arena_pad;
             pg.arena_cached = true;
         }
     }
@@ -471,7 +485,7 @@ int fetch_program(Context &ctx, Program &pg, hipStream_t stream, std::vector<std
 
 void free_program(Context &ctx, Program &pg) {
     for (Executable &ex : pg.parts) free_executable(ctx, ex);
-    if (pg.arena && !pg.arena_cached) (void)hipFree(pg.arena);
+    if (pg.arena && !pg.arena_cached) (void)hipFree(static_cast<char *>(pg.arena) - pg.arena_pad);
     put_buffer(ctx, pg.results, pg.results_cap);
     pg = Program{};
 }

@@ -77,6 +77,7 @@ struct Context {
     // unmapping a few hundred GB of HBM costs ~1 s each way, like a caching
     // allocator the context holds on to it until it is destroyed
     void *arena_cache = nullptr;
+    int64_t arena_cache_pad = 0;        // bytes between the hipMalloc'd pointer and arena_cache (alignment)
     int64_t arena_cache_bytes = 0;
     // small device buffers (sources, descriptors, dims pool, metadata, results)
     // kept for reuse: a one-shot call otherwise pays ~10 hipMalloc / hipFree
@@ -141,6 +142,7 @@ struct Program {
     DType dtype = kF64;
     std::vector<Executable> parts;
     void *arena = nullptr;
+    int64_t arena_pad = 0;              // bytes between the hipMalloc'd pointer and arena (alignment)
     int64_t arena_bytes = 0;
     bool arena_cached = false;          // arena is the context's cache (not freed with the program)
     bool arena_reused = false;          // ... and was already allocated before this program
