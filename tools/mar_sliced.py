@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--link-gbs", type=float, nargs="+", default=[64.0])
     ap.add_argument("--latency-us", type=int, default=20, help="per collective (3 per exchange: sync, data)")
     ap.add_argument("--one-rank", action="store_true", help="also time the one-rank tree (reference point)")
+    ap.add_argument("--lanes", type=int, nargs="+", default=[2, 1], help="schedules to time (2: two fronts, 1: one)")
+    ap.add_argument("--no-model", action="store_true", help="time the compute alone (nocopy) only")
     args = ap.parse_args()
     r, c = args.rows, args.cols
     # the run and the plan statistics see the same budget (the plan-only call
@@ -55,14 +57,15 @@ def main():
         print(json.dumps({"instance": "ising%dx%d-col" % (r, c), "ranks": 1, "wall_ms": min(ts), "walls_ms": ts}),
               flush=True)
     for R in args.ranks:
-        for lanes in (1, 0):
+        for nl in args.lanes:
+            lanes = 1 if nl == 2 else 0
             os.environ["BNPP_SLICE_LANES"] = str(lanes)
             _, st = bnpp.plan_tree_sliced(m, 0, R, order=col)
             rec = {"instance": "ising%dx%d-col" % (r, c), "ranks": R, "lanes": 2 if lanes else 1,
                    "entries_per_rank": st[0], "arena_GB": st[1] / 1e9, "buckets": st[3], "exchanges": st[8],
                    "bytes_sent_per_rank_GB": st[9] / 1e9}
             modes = {"nocopy": "loopback-nocopy"}
-            for g in args.link_gbs:
+            for g in ([] if args.no_model else args.link_gbs):
                 modes["model_%g" % g] = "loopback-model:%d:%d" % (int(g * 1000), args.latency_us)
             for name, coll in modes.items():
                 ts = []
@@ -74,7 +77,7 @@ def main():
                 rec[name + "_walls_ms"] = ts
             links = min(R - 1, 7)
             rec.update({"links_per_rank": links, "latency_us": args.latency_us})
-            for g in args.link_gbs:
+            for g in ([] if args.no_model else args.link_gbs):
                 xfer = st[9] / (links * g * 1e9) * 1e3 + st[8] * 3 * args.latency_us * 1e-3
                 rec["xgmi_ms_%g" % g] = xfer
                 rec["serial_projection_ms_%g" % g] = rec["nocopy_ms"] + xfer
