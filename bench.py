@@ -574,14 +574,23 @@ def main():
     if not args.no_mar and not args.no_mar_f64:
         d = dist if world > 1 else None
         mar_f64 = mar_wallclock(ctx, rank, world, d, dev, args.mar_rows, args.mar_cols, "f64", True)
-        mar_f64.pop("_model")
+        marg64 = mar_f64.pop("_model")[3]
+        if mar is not None:
+            # every one of the R x C marginals: the fp32 MAR against this
+            # independent fp64 one (other plan, slots, kernels) -- the
+            # north star's 1e-6 tolerance, at full size
+            marg32 = sliced_in[3]
+            diff = max(max(abs(a - b) for a, b in zip(marg32[t], marg64[t])) for t in marg64)
+            mar["check_vs_fp64"] = {"method": "max |p_fp32 - p_fp64| over every marginal entry", "max_abs_diff": diff,
+                                    "tolerance": 1e-6, "ok": diff <= 1e-6}
         reference_bound(mar_f64, cpu["value"] if cpu else None)
         ctx.trim()
 
     # every check that decides the exit status, before anything can print
     for rec in (mar, mar_f64):
-        if rec and "check" in rec and not rec["check"]["ok"]:
-            ok = False
+        for key in ("check", "check_vs_fp64"):
+            if rec and key in rec and not rec[key]["ok"]:
+                ok = False
     if mar and "secondary" in mar and mar["secondary"].get("ok") is False:
         ok = False
     if fp64 is not None and not fp64["spot_check_exact"]:

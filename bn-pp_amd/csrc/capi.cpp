@@ -1076,7 +1076,14 @@ int bnpp_ctx_destroy(bnpp_ctx *ctx) {
         g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), ctx), g_ctxs.end());
     }
     (void)hipSetDevice(ctx->c.device);
-    evict_cached_job(ctx);
+    {
+        // a bnpp_model_free on another thread may hold this lock while it
+        // evicts the cached job (it collected the context before the erase
+        // above): wait for it, so the job is destroyed once and the lock is
+        // released before the context is deleted
+        std::lock_guard<std::mutex> lk(ctx->cache_mu);
+        evict_cached_job(ctx);
+    }
     if (ctx->c.stream) (void)hipStreamDestroy(ctx->c.stream);
     if (ctx->c.lane_stream) (void)hipStreamDestroy(ctx->c.lane_stream);
     ctx->srcs.clear();

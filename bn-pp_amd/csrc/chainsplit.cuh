@@ -571,10 +571,34 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
             for (int e = 0; e < 16; ++e) lv[e] = gload(lane_at(lb + (int64_t)slab_e(e) * c.d_slab, lo));
         }
     };
+    // The belief of the tile whose rest offset is `to`, from the lam * pi
+    // products its run_tile left in the image: one wave adds each row's 2^F
+    // products in slab order -- the unfused bucket's order (p = lam * pi;
+    // acc = 0; acc += p for s = 0, 1, ...) -- a 2^F-long dependent chain per
+    // row; the barrier after it hands the image back to the next tile.
+    auto bel_sum = [&](int64_t to) {
+        if constexpr (FORM == kChainBwd && DENSE) {
+            if (w == 0) {
+                // (reading the chunks 8 ahead through a register ring measured
+                // the same: the chain, not the LDS latency, is what it costs)
+                T acc = T(0);
+#pragma unroll 4
+                for (int c4 = 0; c4 < N / VE; ++c4) {
+                    const vec_t<T, VE> v = *reinterpret_cast<const vec_t<T, VE> *>(img + lane * ROWB + 16 * c4);
+#pragma unroll
+                    for (int k = 0; k < VE; ++k) acc = acc + v[k];
+                }
+                store_n<T, 1, kNtStore, true>(c.bel + to + lane, &acc);
+                bmax = acc > bmax ? acc : bmax;
+            }
+            lds_barrier();                                 // the image is the next tile's again
+        }
+    };
     // BM (belief mode): 0 = the run forms no belief; 1 = it does and the
     // caller issued the tile's lam loads (one-run launches: before the next
-    // tile's row loads, so waiting for lam leaves those in flight); 2 = check
-    // c.bel at run time and load lam here (multi-run launches)
+    // tile's row loads, so waiting for lam leaves those in flight) and sums the
+    // products later (bel_sum, after it has issued the next tile's loads); 2 =
+    // check c.bel at run time, load lam here and sum here (multi-run launches)
     auto run_tile = [&](auto bmc, T (&t)[16], int64_t out_off, const int32_t (&gb)[F]) {
         constexpr int BM = decltype(bmc)::value;
         if constexpr (FORM == kChainBwd && DENSE && BM == 2) {
@@ -675,25 +699,15 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 if (BM == 1 || (BM == 2 && c.bel)) {
                     // belief of rest entry r = lane: lam * pi per slab s into row r
                     // of the image (free: every wave read its rows before the
-                    // exchange barrier), then one wave adds each row's 2^F
-                    // products in slab order -- the unfused bucket's order
-                    // (p = lam * pi; acc = 0; acc += p for s = 0, 1, ...)
+                    // exchange barrier); summed by bel_sum -- here (BM 2) or by
+                    // the caller once the next tile's loads are in flight (BM 1:
+                    // the chain then overlaps them instead of idling the other
+                    // waves at a barrier with nothing in flight)
 #pragma unroll
                     for (int e = 0; e < 16; ++e)
                         *reinterpret_cast<T *>(img + lane * ROWB + EB * (wsl | slab_e(e))) = lv[e] * t[e];
                     lds_barrier();
-                    if (w == 0) {
-                        T acc = T(0);
-#pragma unroll 4
-                        for (int c4 = 0; c4 < N / VE; ++c4) {
-                            const vec_t<T, VE> v = *reinterpret_cast<const vec_t<T, VE> *>(img + lane * ROWB + 16 * c4);
-#pragma unroll
-                            for (int k = 0; k < VE; ++k) acc = acc + v[k];
-                        }
-                        store_n<T, 1, kNtStore, true>(c.bel + tout + lane, &acc);
-                        bmax = acc > bmax ? acc : bmax;
-                    }
-                    lds_barrier();                         // the image is the next tile's again
+                    if constexpr (BM == 2) bel_sum(tout);
                 }
             } else {
                 const int64_t w0 = readfirstlane64(out_off);
@@ -735,8 +749,13 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
         decode(vb, in_off, out_off, gb);
         issue(in_off, rg);
         __builtin_amdgcn_s_waitcnt(0x0f70);                // vmcnt(0): the first tile's rows
+        // (3) a fused belief's sum (bel_sum) runs one tile late: after the
+        // next tile's lam and row loads are issued, so the wave adding the
+        // products overlaps them (the other waves wait at its barrier with
+        // those loads in flight, not with an idle memory queue)
         auto loop = [&](auto belc) {
             constexpr bool BEL = decltype(belc)::value;
+            int64_t bel_to = -1;                           // the tile whose products wait in the image
             while (true) {
                 T t[16];
 #pragma unroll
@@ -748,11 +767,16 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 const int64_t vbn = vb + gridDim.x;
                 decode(vbn < total_vblocks ? vbn : total_vblocks - 1, in_off, out_off, gb);
                 issue(in_off, rg);
+                if constexpr (BEL) {
+                    if (bel_to >= 0) bel_sum(bel_to);      // uniform
+                }
                 decode(vb, in_off, out_off, gb);
                 run_tile(std::integral_constant<int, BEL ? 1 : 0>{}, t, out_off, gb);
+                if constexpr (BEL) bel_to = tout;
                 vb = vbn;
                 if (vb >= total_vblocks) break;
             }
+            if constexpr (BEL) bel_sum(bel_to);           // the last tile's
         };
         loop(std::integral_constant<bool, DENSE && MODE == 1>{});
     } else if constexpr (MODE != 2) {
