@@ -1700,30 +1700,38 @@ bool plan_bucket_tree_chain(const std::vector<int> &cards, const std::vector<Vie
             } else {
                 sendv = A;
             }
-            const int vx = (int)B.cards.size();                // scratch: n_slices + 1 int64 exponents
-            B.cards.push_back(2 * (n_slices + 1));
+            // scratch: (E_r, exp2_r) int64 pairs of n_slices + 1 ranks (xchg.hip)
+            const int vx = (int)B.cards.size();
+            B.cards.push_back(4 * (n_slices + 1));
             B.rank.push_back(-1);
-            const int X = B.push_xchg({cur}, {vx}, kXchgSync, 0, n_slices);
-            const int Ts = B.push_xchg({cur, B.view(X)}, sendv, kXchgPack, pmode, n_slices);
             const std::vector<int> &within = Sn.empty() ? A : rest;
             std::vector<int> recvv = So;
             recvv.insert(recvv.end(), within.begin(), within.end());
-            const int Tr = B.push_xchg({B.view(Ts)}, recvv, kXchgComm, Sn.empty() ? 1 : 0, n_slices);
-            ++p.n_xchg;
-            const double ssz = (double)table_size(sendv, B.cards);
-            p.xchg_elems += Sn.empty() ? ssz * (n_slices - 1) : ssz * (n_slices - 1) / n_slices;
             std::vector<int> want;
             for (int v : lam_vars[path[pos]])
                 if (!contains(Sn, v)) want.push_back(v);
             want = B.canon(want);
-            if (want == recvv) return B.view(Tr);
             std::vector<int> tl = within;                      // source blocks fastest: a transpose
             tl.insert(tl.end(), So.begin(), So.end());
-            if (want != tl) {
+            if (want != recvv && want != tl) {
                 ok = false;
                 fail_msg = "slicing: the old slice variables are not the slowest or fastest of the message";
                 return cur;
             }
+            // the destination blocks already slowest (pmode 0: the pack would
+            // only scale) and a transpose after the collective anyway (the
+            // backward lane's re-slices, gathers at the chain's ends): the raw
+            // message travels and the unpack scales each source block as it
+            // transposes -- one data pass instead of two, the same arithmetic
+            const bool late_scale = pmode == 0 && sendv == A && want != recvv;
+            const int X = B.push_xchg({cur}, {vx}, kXchgSync, 0, n_slices);
+            const View send = late_scale ? cur : B.view(B.push_xchg({cur, B.view(X)}, sendv, kXchgPack, pmode, n_slices));
+            const int Tr = B.push_xchg({send}, recvv, kXchgComm, Sn.empty() ? 1 : 0, n_slices);
+            ++p.n_xchg;
+            const double ssz = (double)table_size(sendv, B.cards);
+            p.xchg_elems += Sn.empty() ? ssz * (n_slices - 1) : ssz * (n_slices - 1) / n_slices;
+            if (want == recvv) return B.view(Tr);
+            if (late_scale) return B.view(B.push_xchg({B.view(Tr), B.view(X)}, want, kXchgUnpack, 2, n_slices));
             return B.view(B.push_xchg({B.view(Tr)}, want, kXchgUnpack, 1, n_slices));
         };
         // the forward message of the bucket at position q from the previous one's (or none)

@@ -112,14 +112,15 @@ struct BucketSpec {
     bool simple = false;
     // message-sliced runs (plan_bucket_tree_chain with n_slices > 1): one step
     // of a message exchange between ranks, run by the executor, not a kernel
-    // variant -- kXchgSync: all-gather of each rank's scale exponent of in[0]
-    // into out (n_slices + 1 int64 words); kXchgPack: in[0] scaled to the common
-    // exponent (read from in[1]) into out, blocks of the destination ranks
-    // slowest (xchg_mode 0: in[0] already is, 1: they are in[0]'s fastest
-    // variables -- a transpose); kXchgComm: collective from in[0] to out
-    // (xchg_mode 0: all-to-all, 1: all-gather), out's blocks by source rank
-    // slowest; kXchgUnpack: out = in[0] with the source blocks moved from
-    // slowest to fastest (a transpose)
+    // variant -- kXchgSync: all-gather of each rank's (largest true exponent,
+    // exp2) of in[0] into out (2 (n_slices + 1) int64 words); kXchgPack: in[0]
+    // scaled to the common exponent (read from in[1]) into out, blocks of the
+    // destination ranks slowest (xchg_mode 0: in[0] already is, 1: they are
+    // in[0]'s fastest variables -- a transpose); kXchgComm: collective from
+    // in[0] to out (xchg_mode 0: all-to-all, 1: all-gather), out's blocks by
+    // source rank slowest; kXchgUnpack: out = in[0] with the source blocks
+    // moved from slowest to fastest (a transpose; xchg_mode 2: the blocks came
+    // unpacked, and each is scaled to the common exponent read from in[1])
     int xchg = 0;
     int xchg_mode = 0;
     int xchg_blocks = 1;

@@ -227,7 +227,7 @@ static int run_xchg(Context &ctx, Executable &ex, const Schedule::Group &g, hipS
             err = launch_xchg_sync(f32, ex.d_meta, in_t, out_t, R, stream);
             if (err != hipSuccess) break;
             int64_t *x = static_cast<int64_t *>(ex.h_meta[out_t].ptr);
-            return call(0, x + R, x, 8);
+            return call(0, x + 2 * R, x, 16);                // (E_r, exp2_r) of every rank
         }
         case kXchgPack:
             err = launch_xchg_pack(f32, ex.d_meta, in_t, d.in_table[1], out_t, R, mode, sc.table_size[out_t], stream);
@@ -241,7 +241,9 @@ static int run_xchg(Context &ctx, Executable &ex, const Schedule::Group &g, hipS
             break;
         }
         case kXchgUnpack:
-            err = launch_xchg_unpack(f32, ex.d_meta, in_t, out_t, R, sc.table_size[in_t], stream);
+            // mode 2: the pack was skipped, in[1] holds the gathered exponents
+            err = launch_xchg_unpack(f32, ex.d_meta, in_t, mode == 2 ? d.in_table[1] : -1, out_t, R,
+                                     sc.table_size[in_t], stream);
             break;
         default:
             return fail(ctx, hipErrorInvalidValue, "unknown exchange step");

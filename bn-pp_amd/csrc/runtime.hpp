@@ -49,7 +49,8 @@ hipError_t launch_seq_sum(bool f32, const SeqSumArgs &a, hipStream_t stream);
 hipError_t launch_xchg_sync(bool f32, TableMeta *meta, int in_t, int x_t, int R, hipStream_t s);
 hipError_t launch_xchg_pack(bool f32, TableMeta *meta, int in_t, int x_t, int out_t, int R, int mode, int64_t n,
                             hipStream_t s);
-hipError_t launch_xchg_unpack(bool f32, TableMeta *meta, int in_t, int out_t, int R, int64_t n, hipStream_t s);
+hipError_t launch_xchg_unpack(bool f32, TableMeta *meta, int in_t, int x_t, int out_t, int R, int64_t n,
+                              hipStream_t s);
 hipError_t launch_xchg_meta(TableMeta *meta, int in_t, int out_t, hipStream_t s);
 // stream `s` waits `ns` nanoseconds on the device (one sleeping wave)
 hipError_t launch_delay(double ns, hipStream_t s);

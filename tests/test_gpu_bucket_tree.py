@@ -111,8 +111,9 @@ def test_tree_32x32_full_size_consistent_with_conditioned_partitions():
     (16 GiB), the checkpointed chain schedule, split runs of 8.  The reference
     cannot run it, so parity is through size-independent properties: every
     marginal sums to 1, and P(x_t = s) = Z(x_t = s) / Z from conditioned
-    partitions (north-star tolerance 1e-6).  Own context, closed at the end,
-    so its ~250 GB arena does not stay cached beside the session context."""
+    partitions (north-star tolerance 1e-6), and every marginal agrees with the
+    fp64 MAR to 1e-6.  Own context, closed at the end, so its ~275 GB arena
+    does not stay cached beside the session context."""
     c = bnpp.Context(0)
     try:
         m = bnpp.Model.from_dict(synth.ising_grid(32, 32, seed=0))
@@ -125,6 +126,16 @@ def test_tree_32x32_full_size_consistent_with_conditioned_partitions():
         for t in (0, 527):
             lz0 = bnpp.partition(c, m, {t: 0}, "mf", bnpp.F32, order=col)[0]
             assert abs(10 ** (lz0 - lz) - marg[t][0]) < 1e-6, (t, 10 ** (lz0 - lz), marg[t])
+        # every marginal against the same MAR in fp64 (the reference's
+        # precision): another plan (32-GiB messages, five checkpoint slots,
+        # separate belief passes) and other kernels -- 1e-6 over all 2,048
+        # entries; fp64's own Z-ratio check at 1e-11
+        m64, _ = bnpp.marginals_tree(c, m, {}, "mf", bnpp.F64, order=col)
+        diff = max(abs(a - b) for t in range(1024) for a, b in zip(marg[t], m64[t]))
+        assert diff < 1e-6, diff
+        lz64 = bnpp.partition(c, m, {}, "mf", bnpp.F64, order=col)[0]
+        lz0 = bnpp.partition(c, m, {1023: 0}, "mf", bnpp.F64, order=col)[0]
+        assert abs(10 ** (lz0 - lz64) - m64[1023][0]) < 1e-11
     finally:
         c.close()
 
