@@ -3,7 +3,7 @@
 # the default bench line (as the driver runs them) and the bench kernel's trace.
 set -o pipefail
 R=$PWD
-OUT=$R/gpurun_out/final6a
+OUT=$R/gpurun_out/${FINAL_OUT:-final6a}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
