@@ -1649,11 +1649,21 @@ int bnpp_marginals_tree_sliced(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, con
     if (!out || !out_exp2 || !coll) return set_err(BNPP_ERR_INVALID, "null output or collective");
     if (n_ranks < 2) return set_err(BNPP_ERR_INVALID, "sliced runs need n_ranks >= 2 (bnpp_marginals_tree otherwise)");
     double t0 = now_ms();
-    std::unique_ptr<bnpp_job> job;
-    std::unique_lock<std::mutex> lk;
-    if (ctx) lk = std::unique_lock<std::mutex>(ctx->cache_mu, std::try_to_lock);
-    int rc = create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, job,
-                        0, 1, lk.owns_lock(), n_ranks, rank, budget_gb > 0 ? (int64_t)(budget_gb * 1e9) : 0);
+    if (!ctx || !m) return set_err(BNPP_ERR_INVALID, "null context or model");
+    // an identical call (same model, evidence, order, targets, dtype, rank,
+    // world and budget) relaunches the job the previous one planned, as the
+    // one-GPU tree marginals do; the collective is bound per call
+    bnpp_job *job = nullptr;
+    std::unique_lock<std::mutex> lk(ctx->cache_mu, std::try_to_lock);
+    const bool cache_ok = lk.owns_lock();
+    const int64_t fixed = budget_gb > 0 ? (int64_t)(budget_gb * 1e9) : 0;
+    const int64_t budget = fixed ? fixed : memory_budget(ctx, true);
+    const uint64_t key = cache_ok ? call_key(m, 4, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets,
+                                             dtype, rank, n_ranks) : 0;
+    int rc = oneshot_job(ctx, cache_ok, key, budget, [&](std::unique_ptr<bnpp_job> &j) {
+        return create_job(ctx, m, 3, n_ev, ev_vars, ev_vals, heuristic, order, n_order, n_targets, targets, dtype, j,
+                          0, 1, cache_ok, n_ranks, rank, fixed);
+    }, job);
     const double t1 = now_ms();
     if (rc == BNPP_OK) {
         job->pg.hooks.fn = coll;
@@ -1661,9 +1671,9 @@ int bnpp_marginals_tree_sliced(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, con
         rc = from_ctx(ctx, launch_program(ctx->c, job->pg, ctx->c.stream));
     }
     const double t2 = now_ms();
-    if (rc == BNPP_OK) rc = job_results_sliced(job.get(), ctx->c.stream, out, out_exp2);
+    if (rc == BNPP_OK) rc = job_results_sliced(job, ctx->c.stream, out, out_exp2);
     const double t3 = now_ms();
-    if (job) destroy_job(job.release());
+    oneshot_done(ctx, cache_ok, key, budget, job, rc);
     record_call_timing(t0, t1, t2, t3);
     if (std::getenv("BNPP_TIMING"))
         std::fprintf(stderr, "[bnpp] sliced tree marginals (rank %d of %d): create %.1f ms, launch %.1f ms, run+fetch %.1f ms\n",
