@@ -239,7 +239,10 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
  * mantissas (out, sum(card) doubles) times 2^out_exp2[i] per target
  * (out_exp2 = -2^40 for an all-zero share); the marginal is the normalised sum
  * of the shares over the ranks (bnpp.dist.sliced_tree_marginals).  Trees that
- * are not chains, or chains without such windows: BNPP_ERR_UNSUPPORTED. */
+ * are not chains, or chains without such windows: BNPP_ERR_UNSUPPORTED.  As
+ * bnpp_marginals_tree, the planned job stays with the context, and an
+ * identical call (same model, evidence, order, targets, dtype, rank, n_ranks
+ * and budget) relaunches it; coll / user are bound per call. */
 #define BNPP_COLL_ALLGATHER 0
 #define BNPP_COLL_ALLTOALL 1
 typedef int (*bnpp_collective_fn)(void *user, int op, const void *send, void *recv, int64_t bytes, void *stream);
