@@ -305,6 +305,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 #ifndef BNPP_F64_BEL_ALIAS
 #define BNPP_F64_BEL_ALIAS 0
 #endif
+// BNPP_BEL_SUM_LATE=0 (variant builds): the round-5 placement of a one-run
+// launch's belief sum, at the end of its own tile (1: one tile late, bel_sum)
+#ifndef BNPP_BEL_SUM_LATE
+#define BNPP_BEL_SUM_LATE 1
+#endif
 // (fp64 runs of 8 need it in every kernel they have: one-run and multi-run;
 // they form no fused belief, so there is no MODE 1 kernel of them)
 template <typename T, int MODE, int F>
@@ -707,7 +712,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                     for (int e = 0; e < 16; ++e)
                         *reinterpret_cast<T *>(img + lane * ROWB + EB * (wsl | slab_e(e))) = lv[e] * t[e];
                     lds_barrier();
-                    if constexpr (BM == 2) bel_sum(tout);
+                    if constexpr (BM == 2 || (BM == 1 && !BNPP_BEL_SUM_LATE)) bel_sum(tout);
                 }
             } else {
                 const int64_t w0 = readfirstlane64(out_off);
@@ -767,7 +772,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 const int64_t vbn = vb + gridDim.x;
                 decode(vbn < total_vblocks ? vbn : total_vblocks - 1, in_off, out_off, gb);
                 issue(in_off, rg);
-                if constexpr (BEL) {
+                if constexpr (BEL && BNPP_BEL_SUM_LATE) {
                     if (bel_to >= 0) bel_sum(bel_to);      // uniform
                 }
                 decode(vb, in_off, out_off, gb);
@@ -776,7 +781,7 @@ void chain_split_kernel(const BucketDesc *__restrict__ descs, int n_desc, const 
                 vb = vbn;
                 if (vb >= total_vblocks) break;
             }
-            if constexpr (BEL) bel_sum(bel_to);           // the last tile's
+            if constexpr (BEL && BNPP_BEL_SUM_LATE) bel_sum(bel_to);   // the last tile's
         };
         loop(std::integral_constant<bool, DENSE && MODE == 1>{});
     } else if constexpr (MODE != 2) {

@@ -4,7 +4,7 @@
 # the N-rank bench (gloo, sliced MAR from two ranks, CPU baseline).
 set -o pipefail
 R=$PWD
-OUT=$R/gpurun_out/final6b
+OUT=$R/gpurun_out/${FINAL_OUT:-final6b}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
