@@ -39,8 +39,11 @@ ctx = bnpp.Context(0)
 m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=5))
 col = [i * c + j for j in range(c) for i in range(r) if i * c + j not in ev]
 res, st = bdist.sliced_tree_marginals(ctx, m, rank, world, dist, ev, "mf", dt, col)
+# the identical call again: the planned job is relaunched (no planning)
+res2, _ = bdist.sliced_tree_marginals(ctx, m, rank, world, dist, ev, "mf", dt, col)
+relaunch = {"identical": res2 == res, "plan_ms": bnpp.last_timing()["plan_ms"]}
 if rank == 0:
-    print(json.dumps({"marg": res, "stats": st}))
+    print(json.dumps({"marg": res, "stats": st, "relaunch": relaunch}))
 dist.barrier()
 dist.destroy_process_group()
 ctx.close()
@@ -84,6 +87,7 @@ def _run_world(tmp_path, world, r, c, dtype, ev):
 def test_sliced_world_matches_one_rank_tree(ctx, tmp_path, world, r, c, dtype, ev):
     got = _run_world(tmp_path, world, r, c, dtype, ev)
     assert got["stats"]["calls"] > 0                    # the collective carried the exchanges
+    assert got["relaunch"]["identical"] and got["relaunch"]["plan_ms"] == 0.0, got["relaunch"]
     m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=5))
     col = [i * c + j for j in range(c) for i in range(r) if i * c + j not in ev]
     ref, _ = bnpp.marginals_tree(ctx, m, ev, "mf", dtype, order=col)

@@ -402,6 +402,33 @@ def test_plan_tree_sliced_shares_work_and_exchanges():
         bnpp.plan_tree_sliced(bnpp.Model.load(model_path("alarm.uai")), 0, 2)   # not a chain
 
 
+def test_plan_tree_sliced_exchange_steps(capfd):
+    """Every re-slice is one all-gather of the ranks' (exponent, exp2) pairs,
+    one collective and exactly one data pass: a pack (forward messages: the
+    destination blocks must become the slowest -- a transpose that also scales
+    to the common exponent) or, where the blocks already are the slowest and
+    the received message is transposed anyway (backward messages), the raw
+    block travels and the unpack scales each source block (xchg mode 2); no
+    exchange keeps both passes."""
+    r = c = 16
+    m = bnpp.Model.from_dict(synth.ising_grid(r, c, seed=5))
+    col = [i * c + j for j in range(c) for i in range(r)]
+    for R in (2, 4, 8):
+        os.environ["BNPP_DUMP_PLAN"] = "1"
+        capfd.readouterr()
+        try:
+            _, st = bnpp.plan_tree_sliced(m, 0, R, order=col)
+        finally:
+            del os.environ["BNPP_DUMP_PLAN"]
+        err = capfd.readouterr().err
+        steps = {k: len(re.findall(r"xchg kind=%s " % k, err)) for k in "1234"}
+        late = len(re.findall(r"xchg kind=4 mode=2 ", err))
+        n = int(st[8])
+        assert n > 0 and steps["1"] == n and steps["3"] == n, (R, n, steps)
+        assert late > 0 and steps["4"] == late, (R, steps, late)       # every unpack scales
+        assert steps["2"] + late == n, (R, n, steps, late)             # one data pass per exchange
+
+
 def test_checkpoint_search_picks_a_fitting_slot_count():
     """The checkpoint-slot search (k-ary, probes planned in parallel): under
     budgets below the full tree's arena it returns exactly the plan of one
