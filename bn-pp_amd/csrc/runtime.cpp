@@ -4,7 +4,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+
+#include "lane_order.hpp"
 
 namespace bnpp {
 namespace {
@@ -199,6 +203,17 @@ int make_executable(Context &ctx, const DeviceSources &src, Schedule &&s, Execut
                 if (sc.descs[k].flags & kChainBel) prod[sc.descs[k].aux_out] = gi;
             }
         }
+        // the lanes' windows alternate (lane_order.hpp)
+        std::vector<int> lane(ng);
+        std::vector<char> is_x(ng);
+        std::vector<int64_t> work(ng);
+        for (int gi = 0; gi < ng; ++gi) {
+            lane[gi] = sc.groups[gi].lane;
+            is_x[gi] = sc.groups[gi].variant >= kXchgKeyBase;
+            work[gi] = sc.groups[gi].vblocks;
+        }
+        const char *alt = tuning_knob("BNPP_LANE_ALT");
+        ex.g_order = lane_order(lane, is_x, work, ex.g_record, ex.g_wait, n_ev, alt ? std::atof(alt) : kLaneAltDefault);
         ex.events.assign(n_ev, nullptr);
         for (hipEvent_t &e : ex.events)
             if ((err = hipEventCreateWithFlags(&e, hipEventDisableTiming)) != hipSuccess)
@@ -262,7 +277,9 @@ int launch(Context &ctx, Executable &ex, hipStream_t stream, const XchgHooks *ho
     if (lanes && ((err = hipEventRecord(ex.events[0], stream)) != hipSuccess ||
                   (err = hipStreamWaitEvent(ls[1], ex.events[0], 0)) != hipSuccess))
         return fail(ctx, err, "lane start");
-    for (size_t gi = 0; gi < sc.groups.size(); ++gi) {
+    const bool reorder = lanes && ex.g_order.size() == sc.groups.size();
+    for (size_t oi = 0; oi < sc.groups.size(); ++oi) {
+        const size_t gi = reorder ? (size_t)ex.g_order[oi] : oi;
         const Schedule::Group &g = sc.groups[gi];
         hipStream_t st = ls[lanes ? g.lane & 1 : 0];
         if (lanes)

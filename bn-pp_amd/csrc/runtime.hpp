@@ -133,6 +133,9 @@ struct Executable {
     std::vector<hipEvent_t> events;
     std::vector<int> g_record;
     std::vector<std::vector<int>> g_wait;
+    // lanes: the order the groups are enqueued in (empty: schedule order), the
+    // lanes' windows alternating (lane_order.hpp)
+    std::vector<int> g_order;
     size_t cap_meta = 0, cap_meta0 = 0, cap_desc = 0, cap_pool = 0, cap_copies = 0;   // buffer capacities
 };
 

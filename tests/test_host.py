@@ -552,6 +552,22 @@ def test_generic_offset_width_at_4gib_boundary(tmp_path):
     assert "o32 keys ok" in out.stdout
 
 
+def test_two_lane_enqueue_order(tmp_path):
+    """Sliced two-lane schedules are enqueued windows alternately
+    (lane_order.hpp): a permutation keeping each lane's order, every wait on an
+    event recorded earlier, every cross-lane data dependency kept, and without
+    such dependencies lane 1's window k after lane 0's window k and lane 0's
+    window k + 1 after lane 1's window k: tests/cpp/lane_order.cpp, headers only."""
+    import subprocess
+    exe = str(tmp_path / "lane_order")
+    csrc = os.path.join(REPO, "bn-pp_amd", "csrc")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I" + csrc, os.path.join(REPO, "tests", "cpp", "lane_order.cpp"),
+                    "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert "lane order ok" in out.stdout
+
+
 def test_arena_placement_reaches_the_live_peak(capfd):
     """The fp64 32x32 column-sweep tree with four checkpoint slots holds at
     most seven 34.36-GB messages at once (240.79 GB); one best-fit arena
