@@ -182,6 +182,10 @@ struct Factor::PendingSum {
     std::shared_ptr<const std::vector<double>> in;
     uint64_t k = 1, lo = 1;
 };
+// sum_out inputs up to this many entries (32 MiB) are copied for a lazy
+// partition sum; larger ones are summed at once (a kept copy
+// doubled the host memory of a large factor)
+constexpr size_t kLazySumMax = size_t(1) << 22;
 
 Factor::Factor(const Domain *domain, std::vector<double> values, double partition)
     : _domain(domain), _values(std::move(values)), _partition(partition) {}
@@ -301,13 +305,24 @@ Factor Factor::sum_out(const Variable *variable) const {
           "sum_out");
     Factor r(nd, download(out), 0.0);
     auto ps = std::make_shared<PendingSum>();
-    ps->in = std::make_shared<const std::vector<double>>(_values);
     for (unsigned i = 0; i < _domain->width(); ++i)
         if ((*_domain)[i] == variable) {                 // removal by pointer identity (domain.cpp:57)
             ps->k = variable->size();
             ps->lo = 1;
             for (unsigned j = i + 1; j < _domain->width(); ++j) ps->lo *= (*_domain)[j]->size();
         }
+    if (_values.size() > kLazySumMax) {
+        // a large input: its terms summed now (the same order and bits) rather
+        // than a host copy kept until partition() is read
+        const uint64_t k = ps->k, lo = ps->lo, hi = _values.size() / (k * lo);
+        double p = 0;
+        for (uint64_t h = 0; h < hi; ++h)
+            for (uint64_t l = 0; l < lo; ++l)
+                for (uint64_t v = 0; v < k; ++v) p += _values[(h * k + v) * lo + l];
+        r._partition = p;
+        return r;
+    }
+    ps->in = std::make_shared<const std::vector<double>>(_values);
     r._pending = ps;
     return r;
 }

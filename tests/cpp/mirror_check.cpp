@@ -40,6 +40,23 @@ int main(int argc, char **argv) {
     prod *= f;
     prod *= g;
     CHECK(prod.values() == p.values());
+    // sum_out's partition(): the input's terms in (output entry, summed value)
+    // order (factor.cpp:196-208), for an input summed lazily (small) and one
+    // summed at once (2^23 entries, past the mirror's lazy-copy limit)
+    for (unsigned big : {0u, 1u}) {
+        const unsigned nx = 3, ny = big ? 2048 : 5, nz = big ? 1366 : 7;
+        Variable x(0, nx), y(1, ny), z(2, nz);
+        std::vector<double> hv((size_t)nx * ny * nz);
+        for (size_t i = 0; i < hv.size(); ++i) hv[i] = 0.25 + (double)((i * 2654435761u) % 1000) * 1e-3;
+        Factor h(new Domain({&x, &y, &z}), hv, 0.0);
+        Factor hs = h.sum_out(&y);                   // scope (x, z)
+        double want = 0;
+        for (unsigned ix = 0; ix < nx; ++ix)
+            for (unsigned iz = 0; iz < nz; ++iz)
+                for (unsigned iy = 0; iy < ny; ++iy) want += hv[((size_t)ix * ny + iy) * nz + iz];
+        CHECK(hs.partition() == want);
+        CHECK(hs.size() == (size_t)nx * nz);
+    }
 
     // BN::partition / marginals on the reference's grid3x3 fixtures
     std::string path = dir + "/grid3x3.uai", ev_pr = dir + "/grid3x3-PR.uai.evid", ev_mar = dir + "/grid3x3-MAR.uai.evid";
