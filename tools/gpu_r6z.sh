@@ -2,12 +2,13 @@
 # Sliced 32x32 MAR, 8-rank share on one GPU: the lanes' windows alternating
 # (lane_order.hpp, BNPP_LANE_ALT = 1 strict, 0.5 half, 0 free-running as in
 # round 6 before), tuning build lib_knobs, alternated; then the sliced GPU
-# tests and the closing suite / smoke / bench on the product build.
+# tests (alternating, tuning build) and the closing suite / smoke / bench on
+# the product build.
 set -o pipefail
 R=$PWD
 O=$R/gpurun_out/${R6Z_OUT:-r6z}; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_sliced.py > $O/sliced_tests.log 2>&1 || { tail -30 $O/sliced_tests.log; exit 1; }
+BNPP_LIB=$R/bn-pp_amd/lib_knobs/libbnpp.so BNPP_LANE_ALT=1 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_sliced.py > $O/sliced_tests.log 2>&1 || { tail -30 $O/sliced_tests.log; exit 1; }
 tail -1 $O/sliced_tests.log
 i=0
 for a in 0 1 0.5 0 1; do
