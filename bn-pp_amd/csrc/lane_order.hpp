@@ -11,7 +11,7 @@ namespace bnpp {
 // The share of a window's compute the other lane's next window waits for
 // (two-lane sliced schedules): 1 = strict alternation, 0 = none (the lanes
 // free-run).  BNPP_LANE_ALT overrides it in tuning builds.
-constexpr double kLaneAltDefault = 0.0;
+constexpr double kLaneAltDefault = 1.0;
 
 // Two-lane schedules: the order the groups are enqueued in, and the waits that
 // make the lanes' windows alternate.  A lane's window is its compute groups up
