@@ -229,7 +229,8 @@ int bnpp_marginals_tree_part(bnpp_ctx *ctx, const bnpp_model *m, int n_ev, const
  * order, targets and budget_gb (> 0: the device memory in GB the plan must
  * fit, which sets its checkpoint count -- it must agree across ranks, e.g. the
  * smallest free memory; <= 0: this device's).  The collective is called synchronously from this
- * thread, in the same sequence on every rank, and must be complete (or
+ * thread, in the same sequence on every rank (two-lane schedules: the lanes'
+ * windows alternately, each lane on its own stream), and must be complete (or
  * enqueued on `stream`) when it returns:
  *   op BNPP_COLL_ALLGATHER: each rank contributes `bytes` at send; recv gets
  *                           rank r's at recv + r * bytes
