@@ -3,7 +3,7 @@
 # GPU idles while both lanes wait on exchanges.
 set -o pipefail
 R=$PWD
-O=$R/gpurun_out/r6v; mkdir -p $O
+O=$R/gpurun_out/${R6V_OUT:-r6v}; mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/sliced -o sliced --output-format csv -- python3 $R/tools/mar_sliced.py --ranks 8 --lanes 2 --reps 2 > $O/sliced.jsonl 2> $O/sliced.err || { tail -20 $O/sliced.err; exit 1; }
