@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Where a modelled sliced run idles (rocprofv3 kernel trace, tools/gpu_r6v.sh):
-the trace is cut into calls at > 50 ms with no kernel, and for each call this
+the trace is cut into calls at > 50 ms (argv[2]) with no kernel, and for each call this
 prints its span, the time with no working kernel (delay_kernel, which holds a
 stream for an exchange's modelled xGMI time, does not count as work), and how
 much of that idle time has 0 / 1 / 2 lanes inside a delay.
@@ -10,12 +10,15 @@ import csv
 import sys
 
 
+GAP = float(sys.argv[2]) * 1e6 if len(sys.argv) > 2 else 50e6      # ms of no kernel between calls
+
+
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "delay_kernel" in r["Kernel_Name"]) for r in rows)
     calls, cur, mx = [], [ev[0]], ev[0][1]
     for e in ev[1:]:
-        if e[0] - mx > 50e6:
+        if e[0] - mx > GAP:
             calls.append(cur)
             cur = []
         cur.append(e)
